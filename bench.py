@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""Headline benchmark: samples/sec (whole node) of the toy-MLP DDP demo.
+
+Workload (BASELINE.md / SURVEY.md §6): two independent ToyModels (X, Y) trained
+per iteration -- Linear(2,10), 3x Linear(10,10), Linear(10,1), LeakyReLU --
+MSE loss, Adam(lr=1e-3), fp32, per-rank batch 256, DistributedSampler
+shuffle, global mean loss reduced every step.  One "step" = one iteration of
+``demo.py:99-128`` on every rank: sample the batch, forward+backward both
+models, all-reduce gradients, Adam update of both models, reduce the loss.
+
+Scaling: ``weak`` (default) keeps 512 synthetic samples per rank
+(n = 512*W, per-rank batch 256, global batch 256*W);  ``strong`` reproduces
+the reference's fixed 512-sample set (per-rank batch 512/W capped at 256).
+
+Usage: python bench.py --gpus N --steps K --warmup W   (N>1 under torchrun)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry  # noqa: E402
+from distributed_training_pytorch_amd.data.toy_data import ToyData  # noqa: E402
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer  # noqa: E402
+from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC  # noqa: E402
+from distributed_training_pytorch_amd.ops.optim import OptimConfig  # noqa: E402
+from distributed_training_pytorch_amd.utils import dist_env  # noqa: E402
+
+METRIC = "samples/sec (whole node) toy MLP DDP at 1/2/4/8 MI355X; scaling efficiency"
+# Stock PyTorch-ROCm eager DDP re-enactment of the reference loop, measured on
+# MI355X with `bench.py --impl stock` (BASELINE.md "measured baseline");
+# None until measured for that N.
+STOCK_BASELINE = {}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--impl", choices=["native", "stock"], default="native")
+    ap.add_argument("--launch", choices=["persistent", "graph", "eager"], default="persistent")
+    ap.add_argument("--steps-per-launch", type=int, default=1000)
+    ap.add_argument("--comm", choices=["auto", "rccl", "xgmi"], default="auto")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank, world, local_rank = dist_env.init_from_env(single_rank_pg=a.impl == "stock")
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    n = 512 * world if a.scaling == "weak" else 512
+    ds = ToyData(n=n, seed=a.seed)
+
+    if a.impl == "stock":
+        from distributed_training_pytorch_amd.baselines.stock import StockLoop
+
+        runner = StockLoop(ds, dev, batch=a.batch, seed=a.seed)
+        per_rank_batch = min(a.batch, -(-n // world))
+        train = runner.train
+        sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+        cfg_desc = {"launch": "eager", "comm": "rccl DDP + gloo loss reduce" if world > 1 else "none"}
+    else:
+        X, Y = ds.device_tensors(dev)
+        geom = SamplerGeometry(n=n, world=world, rank=rank, batch=a.batch, seed=a.seed)
+        torch.manual_seed(a.seed)
+        init = [ToyModel().flat_params.detach().clone() for _ in range(2)]
+        ecfg = EngineConfig(comm=a.comm, launch=a.launch, steps_per_launch=a.steps_per_launch)
+        runner = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
+        per_rank_batch = geom.batch_size_at(0)
+        train = runner.train
+        sync = runner.synchronize
+        cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm}
+
+    # warmup (untimed)
+    train(a.warmup)
+    sync()
+    dist_env.barrier()
+    sync()
+    t0 = time.perf_counter()
+    train(a.steps)
+    sync()
+    dist_env.barrier()
+    t1 = time.perf_counter()
+    elapsed = dist_env.allreduce_max(t1 - t0, dev)
+    ms_per_step = 1e3 * elapsed / a.steps
+    total_samples = dist_env.allreduce_sum(float(per_rank_batch * a.steps), dev)
+    value = total_samples / elapsed
+
+    final_loss = None
+    if a.impl == "native":
+        final_loss = runner.losses(runner.t - 1, runner.t)[0].tolist()
+        runner.close()
+    else:
+        final_loss = list(runner.last)
+        runner.close()
+
+    base = STOCK_BASELINE.get(world)
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": (value / base) if (base and a.impl == "native") else None,
+            "dtype": "fp32",
+            "data": "synthetic (ToyData distribution, seeded; random-init ToyModel weights)",
+            "config": {
+                "model": "2x ToyModel MLP 2-10-10-10-10-1 LeakyReLU (X,Y), MSE, Adam lr=1e-3",
+                "global_batch": per_rank_batch * world,
+                "per_rank_batch": per_rank_batch,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "impl": a.impl,
+                "dataset_samples": n,
+                **cfg_desc,
+            },
+            "final_loss": final_loss,
+        }
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

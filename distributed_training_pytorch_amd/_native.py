@@ -1,0 +1,231 @@
+"""ctypes binding of ``_lib/libdtp.so`` (the HIP/CDNA4 kernels + native runtime).
+
+The library has a plain C ABI (``csrc/dtp_api.h``); the ``ctypes.Structure``
+mirrors below must match it field for field.
+
+Policy: on a machine with a GPU the native path is REQUIRED — every op that has
+a HIP kernel raises ``NativeUnavailable`` instead of silently falling back to
+PyTorch when the library is missing.  CPU tensors (the gloo test paths) use the
+PyTorch reference implementations in ``ops/``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  -- must be imported first: libdtp.so binds to torch's HIP runtime
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libdtp.so"
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_double = ctypes.c_double
+c_void_p = ctypes.c_void_p
+c_size_t = ctypes.c_size_t
+c_longlong = ctypes.c_longlong
+c_uint64 = ctypes.c_uint64
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class SamplerCfg(ctypes.Structure):
+    _fields_ = [
+        ("mode", c_int),
+        ("n", c_int),
+        ("world", c_int),
+        ("rank", c_int),
+        ("batch", c_int),
+        ("num_samples", c_int),
+        ("steps_per_epoch", c_int),
+        ("half_bits", c_int),
+        ("seed", c_uint64),
+    ]
+
+
+class Hyper(ctypes.Structure):
+    _fields_ = [
+        ("lr", c_double),
+        ("beta1", c_double),
+        ("beta2", c_double),
+        ("eps", c_double),
+        ("weight_decay", c_double),
+        ("momentum", c_double),
+        ("slope", c_float),
+        ("grad_scale", c_float),
+    ]
+
+
+class TrainArgs(ctypes.Structure):
+    _fields_ = [
+        ("X", c_void_p),
+        ("Y", c_void_p),
+        ("idx", c_void_p),
+        ("params", c_void_p),
+        ("opt_m", c_void_p),
+        ("opt_v", c_void_p),
+        ("step", c_void_p),
+        ("grad_out", c_void_p),
+        ("loss_log", c_void_p),
+        ("status", c_void_p),
+        ("peers", c_void_p),
+        ("epoch", c_void_p),
+        ("loss_log_cap", c_int),
+        ("n_models", c_int),
+        ("n_steps", c_int),
+        ("loss", c_int),
+        ("cache_data", c_int),
+        ("timeout_us", c_int),
+        ("smp", SamplerCfg),
+        ("hp", Hyper),
+    ]
+
+
+class StageArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p),
+        ("params", c_void_p),
+        ("out", c_void_p),
+        ("saved", c_void_p),
+        ("grad_out", c_void_p),
+        ("grad_in", c_void_p),
+        ("grad_params", c_void_p),
+        ("batch", c_int),
+        ("slope", c_float),
+    ]
+
+
+class OptArgs(ctypes.Structure):
+    _fields_ = [
+        ("params", c_void_p),
+        ("opt_m", c_void_p),
+        ("opt_v", c_void_p),
+        ("step", c_void_p),
+        ("grad", c_void_p),
+        ("loss_log", c_void_p),
+        ("loss_log_cap", c_int),
+        ("n_models", c_int),
+        ("P", c_int),
+        ("kind", c_int),
+        ("loss_scale", c_float),
+        ("pad_", c_int),
+        ("hp", Hyper),
+    ]
+
+
+MODE_GRAD, MODE_ADAM, MODE_SGD, MODE_XGMI_ADAM, MODE_XGMI_SGD = 0, 1, 2, 3, 4
+LOSS_MSE, LOSS_CE = 0, 1
+SAMPLER_EXPLICIT, SAMPLER_DIST_SHUFFLE, SAMPLER_SEQUENTIAL, SAMPLER_DIST_NOSHUFFLE = 0, 1, 2, 3
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(lib):
+    P = ctypes.POINTER
+    sig = {
+        "dtp_version": (c_int, []),
+        "dtp_last_error": (ctypes.c_char_p, []),
+        "dtp_runtime_last_error": (ctypes.c_char_p, []),
+        "dtp_mlp_supported": (c_int, [c_int] * 5),
+        "dtp_mlp_param_count": (c_int, [c_int] * 4),
+        "dtp_mlp_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
+        "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
+        "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
+        "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
+        "dtp_sampler_indices": (c_int, [P(SamplerCfg), c_longlong, c_int, c_void_p, c_void_p]),
+        "dtp_get_device": (c_int, [P(c_int)]),
+        "dtp_device_count": (c_int, [P(c_int)]),
+        "dtp_malloc_uncached": (c_int, [c_size_t, P(c_void_p)]),
+        "dtp_malloc": (c_int, [c_size_t, P(c_void_p)]),
+        "dtp_free": (c_int, [c_void_p]),
+        "dtp_ipc_handle_size": (c_int, []),
+        "dtp_ipc_get_handle": (c_int, [c_void_p, c_void_p]),
+        "dtp_ipc_open_handle": (c_int, [c_void_p, P(c_void_p)]),
+        "dtp_ipc_close_handle": (c_int, [c_void_p]),
+        "dtp_can_access_peer": (c_int, [c_int, c_int, P(c_int)]),
+        "dtp_enable_peer_access": (c_int, [c_int]),
+        "dtp_memcpy_peer_async": (c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_void_p]),
+        "dtp_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "dtp_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "dtp_stream_sync": (c_int, [c_void_p]),
+        "dtp_graph_capture_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                            P(c_void_p)]),
+        "dtp_graph_launch": (c_int, [c_void_p, c_void_p]),
+        "dtp_graph_destroy": (c_int, [c_void_p]),
+        "dtp_struct_sizes": (c_int, [P(c_int)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load(build_if_missing: bool = False):
+    """Load libdtp.so (optionally building it first). Raises NativeUnavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists() and build_if_missing:
+            from . import build as _build
+
+            _build.build()
+        if not LIB_PATH.exists():
+            raise NativeUnavailable(
+                f"{LIB_PATH} is missing: build it with `python -m distributed_training_pytorch_amd.build` "
+                "(hipcc --offload-arch=gfx950)")
+        try:
+            lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover
+            raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        _declare(lib)
+        sizes = (c_int * 8)()
+        lib.dtp_struct_sizes(sizes)
+        mine = [ctypes.sizeof(t) for t in (SamplerCfg, Hyper, TrainArgs, StageArgs, OptArgs)]
+        if list(sizes[:5]) != mine:
+            raise NativeUnavailable(f"ABI mismatch between libdtp.so {list(sizes[:5])} and _native.py {mine}: rebuild")
+        _lib = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except NativeUnavailable:
+        return False
+
+
+def require(device: torch.device | None = None):
+    """Return the library for a GPU op; raise loudly if it cannot be loaded."""
+    try:
+        return load()
+    except NativeUnavailable as e:
+        raise NativeUnavailable(f"native HIP kernels are required on {device or 'GPU'}: {e}") from e
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        lib = load()
+        msg = (lib.dtp_last_error() or b"").decode() or (lib.dtp_runtime_last_error() or b"").decode()
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
+
+
+def stream_ptr(stream: torch.cuda.Stream | None = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else int(t.data_ptr())
+
+
+def native_enabled() -> bool:
+    """DTP_NATIVE=0 forces the PyTorch reference path (debug only; never on a timed run)."""
+    return os.environ.get("DTP_NATIVE", "1") != "0"

@@ -1,0 +1,103 @@
+"""Build the native library ``_lib/libdtp.so`` with hipcc for gfx950.
+
+Every ``csrc/*.hip`` file is compiled separately (``hipcc -c``, parallel) and
+linked into one shared object with a plain C ABI, loaded through ctypes by
+``_native.py``.  Built in-tree so the ``.so`` travels with the repository
+snapshot to the GPU box.  No hipify, no CUDA sources: the kernels are written
+for CDNA4 directly.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIBDIR = PKG / "_lib"
+OBJDIR = LIBDIR / "obj"
+LIB = LIBDIR / "libdtp.so"
+ARCH = os.environ.get("DTP_OFFLOAD_ARCH", "gfx950")
+
+COMMON_FLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"--offload-arch={ARCH}",
+    "-mcode-object-version=5",
+    "-Wno-unused-result",
+    "-Wno-unused-command-line-argument",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: install ROCm or set HIPCC")
+
+
+def _sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.glob("*.h"))
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(src: Path, verbose: bool) -> Path:
+    obj = OBJDIR / (src.stem + ".o")
+    if not _stale(obj, [src, *_headers(), Path(__file__)]):
+        return obj
+    cmd = [hipcc(), *COMMON_FLAGS, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> Path:
+    """Compile (incrementally) and link libdtp.so; returns its path."""
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    srcs = _sources()
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4) // 2), 8)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+    if _stale(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def asm(src_name: str, out_dir: Path | None = None) -> Path:
+    """Emit the device assembly (.s) of one source for inspection."""
+    out_dir = out_dir or (LIBDIR / "asm")
+    out_dir.mkdir(parents=True, exist_ok=True)
+    src = CSRC / src_name
+    cmd = [hipcc(), *COMMON_FLAGS, "-I", str(CSRC), "--cuda-device-only", "-S", str(src),
+           "-o", str(out_dir / (src.stem + ".s"))]
+    subprocess.run(cmd, check=True)
+    return out_dir / (src.stem + ".s")
+
+
+if __name__ == "__main__":
+    p = build(verbose="-v" in sys.argv)
+    print(p)

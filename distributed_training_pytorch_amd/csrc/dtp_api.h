@@ -1,0 +1,93 @@
+// C ABI of libdtp.so (consumed from Python through ctypes; every struct here
+// has a mirror in distributed_training_pytorch_amd/_native.py — keep in sync).
+#pragma once
+#include <stdint.h>
+#include "sampler.h"
+
+extern "C" {
+
+// ---- fused train step (fwd + loss + bwd [+ optimizer]) for n_models MLPs ----
+enum DtpTrainMode : int {
+  DTP_MODE_GRAD = 0,       // write local mean-loss gradients (+ loss) into grad_out; no update
+  DTP_MODE_ADAM = 1,       // fused Adam update (single rank, or grads already global)
+  DTP_MODE_SGD = 2,        // fused SGD(+momentum) update
+  DTP_MODE_XGMI_ADAM = 3,  // in-kernel xGMI all-reduce across ranks, then Adam
+  DTP_MODE_XGMI_SGD = 4,   // in-kernel xGMI all-reduce across ranks, then SGD
+};
+
+enum DtpLoss : int { DTP_LOSS_MSE = 0, DTP_LOSS_CE = 1 };
+
+struct DtpHyper {
+  double lr, beta1, beta2, eps, weight_decay, momentum;
+  float slope;        // LeakyReLU negative slope
+  float grad_scale;   // applied to the summed gradient before the update (1/world for DDP averaging)
+};
+
+struct DtpTrainArgs {
+  const float* X;       // [n][IN] dataset inputs (device resident)
+  const float* Y;       // [n][OUT] targets (MSE) or [n] class ids stored as float (CE)
+  const int* idx;       // SAMPLER_EXPLICIT: [n_steps][batch] dataset indices
+  float* params;        // [n_models][P]
+  float* opt_m;         // [n_models][P] Adam exp_avg / SGD momentum buffer
+  float* opt_v;         // [n_models][P] Adam exp_avg_sq
+  int* step;            // [n_models] optimizer step counters (device side)
+  float* grad_out;      // MODE_GRAD: [n_models][P] gradients then [n_models] mean losses
+  float* loss_log;      // [loss_log_cap][n_models] mean loss per step (nullable)
+  int* status;          // [16] error / timeout words (xGMI mode), nullable
+  float* const* peers;  // MODE_XGMI_*: [world] device pointers of every rank's receive buffer
+  unsigned* epoch;      // MODE_XGMI_*: [n_models] exchange epoch counters (device)
+  int loss_log_cap;
+  int n_models;
+  int n_steps;
+  int loss;             // DtpLoss
+  int cache_data;       // stage the dataset in LDS (persistent multi-step runs)
+  int timeout_us;       // bound on every cross-GPU spin (xGMI)
+  dtp::SamplerCfg smp;
+  DtpHyper hp;
+};
+
+int dtp_version(void);
+const char* dtp_last_error(void);
+int dtp_mlp_supported(int in, int h, int nl, int out, int final_act);
+int dtp_mlp_param_count(int in, int h, int nl, int out);
+int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream);
+
+// ---- stage forward / backward (autograd path, layer-split pipeline) ----
+struct DtpStageArgs {
+  const float* x;         // [B][IN]
+  const float* params;    // [P]
+  float* out;             // [B][OUT]  (forward output; read by backward when FINAL_ACT)
+  float* saved;           // [B][(NL-1)*H] hidden activations
+  const float* grad_out;  // [B][OUT]  (backward)
+  float* grad_in;         // [B][IN]   (backward, nullable)
+  float* grad_params;     // [P]       (backward; must be zeroed when the grid has >1 block)
+  int batch;
+  float slope;
+};
+
+int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);
+int dtp_mlp_stage_bwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);
+
+// ---- flat optimizers over [n_models][P] (after an external all-reduce) ----
+struct DtpOptArgs {
+  float* params;
+  float* opt_m;
+  float* opt_v;
+  int* step;          // [n_models]
+  const float* grad;  // [n_models][P] (+ [n_models] losses when loss_log != null)
+  float* loss_log;
+  int loss_log_cap;
+  int n_models;
+  int P;
+  int kind;           // DTP_MODE_ADAM or DTP_MODE_SGD
+  float loss_scale;   // applied to the all-reduced losses (1/world)
+  int pad_;
+  DtpHyper hp;
+};
+
+int dtp_flat_optimizer(const DtpOptArgs* a, void* stream);
+
+// sampler probe (tests): dataset indices of steps [t0, t0+n_steps), row-major [n_steps][batch], -1 padded
+int dtp_sampler_indices(const dtp::SamplerCfg* s, long long t0, int n_steps, int* out, void* stream);
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// Flat optimizer over [n_models][P] parameters after an external (RCCL)
+// gradient all-reduce: one launch updates every model (the reference runs
+// ~7 elementwise kernels per parameter tensor x 10 tensors x 2 models,
+// SURVEY.md §2.6 K11).  The DDP 1/W averaging and the loss bookkeeping are
+// fused in.
+#include <string>
+
+#include "dtp_api.h"
+#include "optim_core.h"
+
+namespace dtp {
+
+__global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
+  const int model = blockIdx.y;
+  const long long t = a.step[model];
+  float* p = a.params + (size_t)model * a.P;
+  float* m = a.opt_m + (size_t)model * a.P;
+  float* v = a.opt_v ? a.opt_v + (size_t)model * a.P : nullptr;
+  const float* g = a.grad + (size_t)model * a.P;
+  if (a.kind == DTP_MODE_ADAM) {
+    const AdamScalars s = adam_scalars(a.hp, t + 1);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.P; i += gridDim.x * kBlock) {
+      float w = p[i], mi = m[i], vi = v[i];
+      adam_update(w, mi, vi, g[i] * a.hp.grad_scale, s);
+      p[i] = w;
+      m[i] = mi;
+      v[i] = vi;
+    }
+  } else {
+    const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.P; i += gridDim.x * kBlock) {
+      float w = p[i], bi = m[i];
+      sgd_update(w, bi, g[i] * a.hp.grad_scale, lr, mom, wd, t == 0);
+      p[i] = w;
+      m[i] = bi;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (a.loss_log)
+      a.loss_log[(size_t)(t % a.loss_log_cap) * a.n_models + model] = a.grad[(size_t)a.n_models * a.P + model] * a.loss_scale;
+  }
+  // the step counter is read by every block of this model: advance it only
+  // after the grid is done -> done by the last block via a ticket would cost a
+  // fence; instead the counter is advanced by a 1-block follow-up in the same
+  // stream when gridDim.x > 1 (see launcher).
+  if (gridDim.x == 1 && threadIdx.x == 0) a.step[model] = (int)(t + 1);
+}
+
+__global__ void advance_steps_kernel(int* step, int n) {
+  const int i = threadIdx.x;
+  if (i < n) step[i] += 1;
+}
+
+}  // namespace dtp
+
+namespace {
+thread_local std::string g_opt_err;
+}
+
+extern "C" int dtp_flat_optimizer(const DtpOptArgs* a, void* stream) {
+  if (!a || a->P <= 0 || a->n_models <= 0) return -1;
+  if (a->kind != DTP_MODE_ADAM && a->kind != DTP_MODE_SGD) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  int nblk = (a->P + dtp::kBlock - 1) / dtp::kBlock;
+  if (nblk > 1024) nblk = 1024;
+  dim3 grid(nblk, a->n_models), block(dtp::kBlock);
+  hipLaunchKernelGGL(dtp::flat_optimizer_kernel, grid, block, 0, st, *a);
+  if (nblk > 1) hipLaunchKernelGGL(dtp::advance_steps_kernel, dim3(1), dim3(64), 0, st, a->step, a->n_models);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

@@ -1,0 +1,49 @@
+// Optimizer math shared by the fused train-step kernel and the flat optimizer
+// kernel.  Mirrors torch.optim.Adam / torch.optim.SGD (defaults used by the
+// reference: Adam(lr=1e-3), demo.py:80-81) element for element:
+//   Adam:  m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+//          denom = sqrt(v)/sqrt(1-b2^t) + eps; p.addcdiv_(m, denom, -lr/(1-b1^t))
+//   SGD :  buf = g (first step) | buf*mom + g;  p.add_(buf, -lr)
+// with the scalar bias corrections formed in double, as torch does on the host.
+#pragma once
+#include "dtp_api.h"
+#include "dtp_common.h"
+
+namespace dtp {
+
+struct AdamScalars {
+  float step_size, bc2_sqrt, one_m_b1, b2, one_m_b2, eps, wd;
+};
+
+DTP_DEV AdamScalars adam_scalars(const DtpHyper& hp, long long t1) {
+  AdamScalars s;
+  const double bc1 = 1.0 - pow_int(hp.beta1, (uint64_t)t1);
+  const double bc2 = 1.0 - pow_int(hp.beta2, (uint64_t)t1);
+  s.step_size = (float)(hp.lr / bc1);
+  s.bc2_sqrt = (float)sqrt(bc2);
+  s.one_m_b1 = (float)(1.0 - hp.beta1);
+  s.b2 = (float)hp.beta2;
+  s.one_m_b2 = (float)(1.0 - hp.beta2);
+  s.eps = (float)hp.eps;
+  s.wd = (float)hp.weight_decay;
+  return s;
+}
+
+DTP_DEV void adam_update(float& p, float& m, float& v, float g, const AdamScalars& s) {
+  if (s.wd != 0.f) g = g + s.wd * p;
+  m = m + s.one_m_b1 * (g - m);
+  v = v * s.b2 + s.one_m_b2 * g * g;
+  const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
+  p = p - s.step_size * (m / denom);
+}
+
+DTP_DEV void sgd_update(float& p, float& buf, float g, float lr, float mom, float wd, bool first) {
+  if (wd != 0.f) g = g + wd * p;
+  if (mom != 0.f) {
+    buf = first ? g : buf * mom + g;
+    g = buf;
+  }
+  p = p - lr * g;
+}
+
+}  // namespace dtp

@@ -1,0 +1,318 @@
+"""FusedTrainer: the MI355X-native training engine for small MLP families.
+
+One training iteration of the reference (``demo.py:95-129``: sampler ->
+H2D -> fwd X, fwd Y -> MSE -> backward (DDP all-reduce) -> Adam x2 -> loss
+all-reduce over gloo) becomes, per rank:
+
+* ``comm="none"`` (W == 1):  ONE kernel launch for ``steps_per_launch``
+  iterations of both models (persistent: weights, Adam state and the 6 KB
+  dataset stay in LDS/registers), or a hipGraph of single-step launches.
+* ``comm="rccl"``: fused grad kernel -> ``all_reduce`` of ONE flat buffer
+  holding both models' gradients AND the two losses (RCCL over xGMI) ->
+  fused flat-optimizer kernel.  Optionally captured into a hipGraph.
+* ``comm="xgmi"``: ONE persistent kernel per ``steps_per_launch`` iterations;
+  the all-reduce happens inside the step through peer-mapped xGMI buffers
+  (``parallel/xgmi.py``).
+* CPU tensors: the PyTorch reference of exactly the same step (gloo all-reduce).
+
+The loss is never synchronised to the host inside the loop: every step writes
+its global mean loss into a device ring (``loss_log``) read lazily.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from .. import _native as nat
+from ..data.sampler import EpochIndexStream, SamplerGeometry
+from ..ops.mlp import MlpSpec, mlp_forward_ref
+from ..ops.optim import OptimConfig, adam_update_ref, flat_optimizer_step, sgd_update_ref
+
+
+@dataclass
+class EngineConfig:
+    comm: str = "auto"           # auto | none | rccl | xgmi | gloo
+    launch: str = "persistent"   # persistent | graph | eager
+    steps_per_launch: int = 1000  # persistent: iterations per kernel; graph: launches per graph
+    sampler: str = "device"      # device (in-kernel Feistel) | torch (exact DistributedSampler order)
+    loss: str = "mse"            # mse | ce
+    log_cap: int = 1 << 16
+    cache_data: bool = True
+    xgmi_timeout_us: int = 20_000_000
+    rccl_graph: bool = True      # capture grad->all_reduce->optimizer into a hipGraph
+
+
+class FusedTrainer:
+    def __init__(self, spec: MlpSpec, n_models: int, X: torch.Tensor, Y: torch.Tensor,
+                 geom: SamplerGeometry, optim: OptimConfig | None = None,
+                 cfg: EngineConfig | None = None, init_params: list[torch.Tensor] | None = None,
+                 group=None):
+        self.spec = spec
+        self.n_models = n_models
+        self.optim = optim or OptimConfig()
+        self.cfg = cfg or EngineConfig()
+        self.geom = geom
+        self.group = group
+        self.device = X.device
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if geom.world != self.world or geom.rank != self.rank:
+            raise ValueError(f"sampler geometry ({geom.rank}/{geom.world}) does not match the process group "
+                             f"({self.rank}/{self.world})")
+        self.X = X.contiguous().float()
+        self.Y = Y.contiguous().float()
+        P = spec.P
+        dev = self.device
+        self.params = torch.empty(n_models, P, device=dev, dtype=torch.float32)
+        if init_params is not None:
+            for i, p in enumerate(init_params):
+                self.params[i].copy_(p.reshape(-1))
+        else:
+            self.params.normal_(0, 0.3)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.step_ctr = torch.zeros(n_models, dtype=torch.int32, device=dev)
+        self.loss_log = torch.zeros(self.cfg.log_cap, n_models, dtype=torch.float32, device=dev)
+        self.comm_buf = torch.zeros(n_models * P + n_models, dtype=torch.float32, device=dev)
+        self.t = 0  # host mirror of the step counter
+        self._idx_stream = EpochIndexStream(geom)
+        self._graphs: dict = {}
+        self._xgmi = None
+        self.comm = self._resolve_comm()
+        # DDP construction semantics: every rank starts from rank 0's weights
+        if self.world > 1:
+            dist.broadcast(self.params, src=0, group=group)
+        self.native = self.device.type == "cuda" and nat.native_enabled()
+        if self.native:
+            nat.require(self.device)
+            if not spec.native_supported():
+                raise NotImplementedError(f"no fused kernel for {spec}")
+        if self.comm == "xgmi":
+            from ..parallel.xgmi import XgmiExchange
+
+            self._xgmi = XgmiExchange(n_models, P, dev, group)
+
+    # ------------------------------------------------------------------ setup
+    def _resolve_comm(self) -> str:
+        c = self.cfg.comm
+        if self.world == 1:
+            return "none"
+        if self.device.type != "cuda":
+            return "gloo"
+        if c == "auto":
+            return "rccl"
+        if c not in ("rccl", "xgmi"):
+            raise ValueError(f"comm {c!r} not valid for a GPU run with world={self.world}")
+        return c
+
+    def _hyper(self, grad_scale: float) -> nat.Hyper:
+        return self.optim.hyper(self.spec.slope, grad_scale)
+
+    def _train_args(self, n_steps: int, mode: int, idx: torch.Tensor | None, batch_override: int | None = None):
+        g = self.geom
+        smp = g.to_native()
+        if idx is not None:
+            smp.mode = nat.SAMPLER_EXPLICIT
+            smp.batch = batch_override or g.batch
+        xg = self._xgmi
+        return nat.TrainArgs(
+            nat.ptr(self.X), nat.ptr(self.Y), nat.ptr(idx), nat.ptr(self.params), nat.ptr(self.m), nat.ptr(self.v),
+            nat.ptr(self.step_ctr), nat.ptr(self.comm_buf), nat.ptr(self.loss_log),
+            nat.ptr(xg.status) if xg else None, nat.ptr(xg.peer_table) if xg else None,
+            nat.ptr(xg.epoch) if xg else None,
+            self.loss_log.shape[0], self.n_models, n_steps,
+            nat.LOSS_CE if self.cfg.loss == "ce" else nat.LOSS_MSE,
+            int(self.cfg.cache_data), self.cfg.xgmi_timeout_us, smp,
+            # xGMI modes sum the W gradients in-kernel -> DDP averaging 1/W there;
+            # MODE_GRAD writes local means (the flat optimizer applies 1/W)
+            self._hyper(1.0 / self.world if mode in (nat.MODE_XGMI_ADAM, nat.MODE_XGMI_SGD) else 1.0))
+
+    def _update_mode(self) -> int:
+        if self.comm == "xgmi":
+            return nat.MODE_XGMI_ADAM if self.optim.name == "adam" else nat.MODE_XGMI_SGD
+        return self.optim.kind
+
+    # ------------------------------------------------------------------ steps
+    def train(self, n_steps: int) -> None:
+        """Run n_steps training iterations (asynchronous on the GPU)."""
+        if n_steps <= 0:
+            return
+        if not self.native:
+            for _ in range(n_steps):
+                self._reference_step()
+            return
+        if self.comm == "rccl":
+            for _ in range(n_steps):
+                self._rccl_step()
+            return
+        remaining = n_steps
+        while remaining > 0:
+            if self.cfg.sampler == "torch":
+                k = self._explicit_chunk(remaining)
+                self._launch_explicit(k)
+            elif self.cfg.launch == "persistent":
+                k = min(remaining, self.cfg.steps_per_launch)
+                self._launch(k)
+            elif self.cfg.launch == "graph":
+                G = self.cfg.steps_per_launch
+                if remaining >= G:
+                    self._graph_launch(G)
+                    k = G
+                else:
+                    k = 1
+                    self._launch(1)
+            else:
+                k = 1
+                self._launch(1)
+            remaining -= k
+            self.t += k
+
+    def _launch(self, k: int, idx: torch.Tensor | None = None, batch_override: int | None = None):
+        lib = nat.load()
+        a = self._train_args(k, self._update_mode(), idx, batch_override)
+        nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], self._update_mode(), nat.stream_ptr()),
+                  "dtp_mlp_train")
+
+    def _graph_launch(self, G: int):
+        lib = nat.load()
+        key = ("train", G)
+        h = self._graphs.get(key)
+        if h is None:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            a = self._train_args(1, self._update_mode(), None)
+            hp = ctypes.c_void_p()
+            nat.check(lib.dtp_graph_capture_train(ctypes.byref(a), *self.spec.key[:4], self._update_mode(), G,
+                                                  nat.stream_ptr(s), ctypes.byref(hp)), "dtp_graph_capture_train")
+            torch.cuda.current_stream().wait_stream(s)
+            h = hp.value
+            self._graphs[key] = h
+        nat.check(lib.dtp_graph_launch(ctypes.c_void_p(h), nat.stream_ptr()), "dtp_graph_launch")
+
+    def _explicit_chunk(self, remaining: int) -> int:
+        # steps with the same batch size can share one launch
+        k = 0
+        b0 = self.geom.batch_size_at(self.t)
+        while k < min(remaining, self.cfg.steps_per_launch) and self.geom.batch_size_at(self.t + k) == b0:
+            k += 1
+        return k
+
+    def _launch_explicit(self, k: int):
+        b0 = self.geom.batch_size_at(self.t)
+        rows = [self._idx_stream.indices(self.t + i) for i in range(k)]
+        idx = torch.tensor(rows, dtype=torch.int32).pin_memory().to(self.device, non_blocking=True)
+        self._launch(k, idx, b0)
+        self._keepalive = idx
+
+    def _rccl_step(self):
+        lib = nat.load()
+        if self.cfg.rccl_graph:
+            g = self._graphs.get("rccl")
+            if g is None:
+                g = self._capture_rccl()
+            if g is not False:
+                g.replay()
+                self.t += 1
+                return
+        self._rccl_body(lib)
+        self.t += 1
+
+    def _rccl_body(self, lib, idx=None):
+        a = self._train_args(1, nat.MODE_GRAD, idx)
+        nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
+                  "dtp_mlp_train(grad)")
+        dist.all_reduce(self.comm_buf, group=self.group)
+        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, self.comm_buf, self.optim,
+                            grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world,
+                            slope=self.spec.slope)
+
+    def _capture_rccl(self):
+        lib = nat.load()
+        # warm the communicator outside capture, then capture one whole step
+        try:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._rccl_body(lib)  # eager warm-up step (counts as a real step)
+            torch.cuda.current_stream().wait_stream(s)
+            self.t += 1
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._rccl_body(lib)
+            self._graphs["rccl"] = g
+            return g
+        except Exception as e:  # capture of collectives unsupported -> eager
+            print(f"[dtp] hipGraph capture of the RCCL step failed ({e}); running eager", flush=True)
+            self._graphs["rccl"] = False
+            return False
+
+    # ------------------------------------------------------------------ CPU reference path
+    def _reference_step(self):
+        g = self.geom
+        idx = torch.tensor(self._idx_stream.indices(self.t) if self.cfg.sampler == "torch" else g.indices(self.t),
+                           dtype=torch.long, device=self.device)
+        x, y = self.X[idx], self.Y[idx]
+        grads = []
+        losses = []
+        for i in range(self.n_models):
+            p = self.params[i].detach().clone().requires_grad_(True)
+            out = mlp_forward_ref(p, self.spec, x)
+            if self.cfg.loss == "ce":
+                loss = torch.nn.functional.cross_entropy(out, y.view(-1).long())
+            else:
+                loss = torch.nn.functional.mse_loss(out, y.view_as(out))
+            (gp,) = torch.autograd.grad(loss, p)
+            grads.append(gp)
+            losses.append(loss.detach().reshape(1))
+        buf = torch.cat([torch.stack(grads).reshape(-1), torch.cat(losses)])
+        if self.world > 1:
+            dist.all_reduce(buf, group=self.group)
+        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.optim,
+                            grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world)
+        self.t += 1
+
+    # ------------------------------------------------------------------ state / logging
+    def synchronize(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        if self._xgmi is not None:
+            self._xgmi.check_status()
+
+    def losses(self, t0: int, t1: int) -> torch.Tensor:
+        """Global mean losses of steps [t0, t1) as a CPU tensor [t1-t0, n_models] (syncs)."""
+        cap = self.loss_log.shape[0]
+        if t1 - t0 > cap:
+            t0 = t1 - cap
+        ids = torch.arange(t0, t1) % cap
+        return self.loss_log.index_select(0, ids.to(self.loss_log.device)).cpu()
+
+    def state_dict(self) -> dict:
+        return {"params": self.params.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(),
+                "step": self.step_ctr.cpu(), "t": self.t, "spec": self.spec.__dict__,
+                "optim": self.optim.__dict__}
+
+    def load_state_dict(self, sd: dict):
+        self.params.copy_(sd["params"])
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.step_ctr.copy_(sd["step"])
+        self.t = int(sd["t"])
+
+    def model_params(self, i: int) -> torch.Tensor:
+        return self.params[i]
+
+    def close(self):
+        lib = nat.load() if self.native else None
+        for k, h in list(self._graphs.items()):
+            if isinstance(h, int) and lib is not None:
+                lib.dtp_graph_destroy(ctypes.c_void_p(h))
+        self._graphs.clear()
+        if self._xgmi is not None:
+            if dist.is_initialized():
+                dist.barrier(group=self.group)
+            self._xgmi.close()
+            self._xgmi = None

@@ -1,0 +1,62 @@
+"""ToyModel: the reference's 5-layer LeakyReLU MLP (``toy_model_and_data.py:8-25``),
+built for the fused HIP path.
+
+* Same module tree and ``state_dict`` keys as the reference
+  (``layers.{0,2,4,6,8}.{weight,bias}``), so checkpoints interchange.
+* All parameters are views into ONE contiguous fp32 buffer (``flat_params``) in
+  ``parameters()`` order -- the layout every kernel and the flat DDP all-reduce
+  use.  The packing survives ``.to()/.cuda()`` (re-flattened in ``_apply``).
+* On a CUDA input the forward is ONE fused kernel and the backward ONE fused
+  kernel (``ops.mlp.FusedMLPFunction``); on CPU it is plain PyTorch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops.mlp import MlpSpec, fused_mlp
+
+
+class ToyModel(nn.Module):
+    def __init__(self, in_features: int = 2, hidden: int = 10, depth: int = 3, out_features: int = 1,
+                 slope: float = 0.01):
+        super().__init__()
+        self.spec = MlpSpec(in_features, hidden, depth + 2, out_features, False, slope)
+        mods: list[nn.Module] = [nn.Linear(in_features, hidden), nn.LeakyReLU(slope)]
+        for _ in range(depth):
+            mods += [nn.Linear(hidden, hidden), nn.LeakyReLU(slope)]
+        mods.append(nn.Linear(hidden, out_features))
+        self.layers = nn.Sequential(*mods)
+        self.flatten_parameters()
+
+    # -- flat parameter packing ------------------------------------------------
+    def flatten_parameters(self) -> torch.Tensor:
+        ps = list(self.layers.parameters())
+        if ps:
+            flat = torch.empty(sum(p.numel() for p in ps), dtype=ps[0].dtype, device=ps[0].device)
+            o = 0
+            for p in ps:
+                n = p.numel()
+                flat[o:o + n].copy_(p.data.reshape(-1))
+                p.data = flat[o:o + n].view_as(p)
+                o += n
+            self._flat = flat
+        return self._flat
+
+    @property
+    def flat_params(self) -> torch.Tensor:
+        return self._flat
+
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        self.flatten_parameters()
+        return out
+
+    def load_flat_(self, flat: torch.Tensor) -> None:
+        with torch.no_grad():
+            self._flat.copy_(flat.reshape(-1).to(self._flat))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            return fused_mlp(x, self.spec, list(self.layers.parameters()))
+        return self.layers(x)

@@ -1,0 +1,206 @@
+"""Fused MLP ops: spec, PyTorch reference, native HIP wrappers, autograd Function.
+
+The toy network of the reference (``toy_model_and_data.py:8-25``: Linear(2,10),
+LeakyReLU, 3x[Linear(10,10), LeakyReLU], Linear(10,1)) is described by an
+:class:`MlpSpec`.  Parameters live in ONE flat fp32 buffer in torch's
+``parameters()`` order (W0, b0, W1, b1, ...), which is what every kernel reads
+and what the data-parallel all-reduce moves in a single message.
+
+CUDA tensors go through the HIP kernels in ``csrc/mlp_train.hip``;
+CPU tensors (gloo tests, ``--device cpu``) through the PyTorch reference below.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, replace
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native as nat
+
+
+@dataclass(frozen=True)
+class MlpSpec:
+    in_features: int = 2
+    hidden: int = 10
+    n_layers: int = 5
+    out_features: int = 1
+    final_act: bool = False
+    slope: float = 0.01
+
+    def dims(self) -> list[tuple[int, int]]:
+        out = []
+        for l in range(self.n_layers):
+            din = self.in_features if l == 0 else self.hidden
+            dout = self.out_features if l == self.n_layers - 1 else self.hidden
+            out.append((din, dout))
+        return out
+
+    @property
+    def P(self) -> int:
+        return sum(o * (i + 1) for i, o in self.dims())
+
+    def param_shapes(self) -> list[tuple[int, ...]]:
+        shapes: list[tuple[int, ...]] = []
+        for i, o in self.dims():
+            shapes += [(o, i), (o,)]
+        return shapes
+
+    def act(self, l: int) -> bool:
+        return l < self.n_layers - 1 or self.final_act
+
+    def substage(self, a: int, b: int) -> "MlpSpec":
+        """Spec of layers a..b (inclusive) as a stand-alone stage."""
+        dims = self.dims()
+        return replace(self, in_features=dims[a][0], out_features=dims[b][1], n_layers=b - a + 1,
+                       final_act=(b < self.n_layers - 1) or self.final_act)
+
+    def param_range(self, a: int, b: int) -> tuple[int, int]:
+        """Flat-parameter slice [lo, hi) of layers a..b."""
+        dims = self.dims()
+        lo = sum(o * (i + 1) for i, o in dims[:a])
+        hi = lo + sum(o * (i + 1) for i, o in dims[a:b + 1])
+        return lo, hi
+
+    @property
+    def key(self) -> tuple[int, int, int, int, int]:
+        return (self.in_features, self.hidden, self.n_layers, self.out_features, int(self.final_act))
+
+    def native_supported(self) -> bool:
+        try:
+            lib = nat.load()
+        except nat.NativeUnavailable:
+            return False
+        return bool(lib.dtp_mlp_supported(*self.key))
+
+
+TOY_SPEC = MlpSpec()
+
+
+# ----------------------------------------------------------------------------- reference
+def unflatten(flat: torch.Tensor, spec: MlpSpec) -> list[torch.Tensor]:
+    out, o = [], 0
+    for shp in spec.param_shapes():
+        n = 1
+        for s in shp:
+            n *= s
+        out.append(flat[o:o + n].view(*shp))
+        o += n
+    return out
+
+
+def mlp_forward_ref(flat: torch.Tensor, spec: MlpSpec, x: torch.Tensor) -> torch.Tensor:
+    ps = unflatten(flat, spec)
+    h = x
+    for l in range(spec.n_layers):
+        h = F.linear(h, ps[2 * l], ps[2 * l + 1])
+        if spec.act(l):
+            h = F.leaky_relu(h, spec.slope)
+    return h
+
+
+# ----------------------------------------------------------------------------- native
+def _check_f32_cuda(name: str, t: torch.Tensor, device: torch.device, numel: int | None = None):
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name} must be on {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} must have {numel} elements, got {t.numel()}")
+
+
+def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool = True):
+    """Native forward of one MLP stage. Returns (out [B,OUT], saved [B,(NL-1)*H] or None)."""
+    lib = nat.require(x.device)
+    if x.dim() != 2 or x.shape[1] != spec.in_features:
+        raise ValueError(f"input must be [B, {spec.in_features}], got {tuple(x.shape)}")
+    dev = x.device
+    _check_f32_cuda("x", x, dev)
+    _check_f32_cuda("params", flat, dev, spec.P)
+    B = x.shape[0]
+    out = torch.empty(B, spec.out_features, device=dev, dtype=torch.float32)
+    saved = torch.empty(B, (spec.n_layers - 1) * spec.hidden, device=dev, dtype=torch.float32) \
+        if (save and spec.n_layers > 1) else None
+    a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), None, None, None, B, spec.slope)
+    nat.check(lib.dtp_mlp_stage_fwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_fwd")
+    return out, saved
+
+
+def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: bool = True):
+    """Native backward of one stage. Returns (grad_in or None, grad_params [P])."""
+    lib = nat.require(x.device)
+    dev = x.device
+    B = x.shape[0]
+    grad_out = grad_out.contiguous()
+    _check_f32_cuda("grad_out", grad_out, dev, B * spec.out_features)
+    grad_in = torch.empty(B, spec.in_features, device=dev, dtype=torch.float32) if need_grad_in else None
+    nblk = (B + 1023) // 1024
+    gp = torch.zeros(spec.P, device=dev, dtype=torch.float32) if nblk > 1 else \
+        torch.empty(spec.P, device=dev, dtype=torch.float32)
+    a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), nat.ptr(grad_out),
+                      nat.ptr(grad_in), nat.ptr(gp), B, spec.slope)
+    nat.check(lib.dtp_mlp_stage_bwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_bwd")
+    return grad_in, gp
+
+
+def _flat_view_of(params: list[torch.Tensor]) -> torch.Tensor | None:
+    """If params are consecutive views of one contiguous storage, return that flat span."""
+    if not params:
+        return None
+    p0 = params[0]
+    base = p0.data_ptr()
+    off = 0
+    for p in params:
+        if not p.is_contiguous() or p.data_ptr() != base + off * 4 or p.dtype != torch.float32:
+            return None
+        off += p.numel()
+    st = p0.untyped_storage()
+    start = (base - st.data_ptr()) // 4
+    full = torch.empty(0, dtype=torch.float32, device=p0.device).set_(st, start, (off,), (1,))
+    return full
+
+
+class FusedMLPFunction(torch.autograd.Function):
+    """y = MLP(x) with the forward and the whole backward (dX chain + MFMA dW
+    reduction) each in ONE kernel, instead of ~9 GEMM + ~10 elementwise launches."""
+
+    @staticmethod
+    def forward(ctx, x, spec: MlpSpec, *params):
+        flat = _flat_view_of(list(params))
+        if flat is None:
+            flat = torch.cat([p.detach().reshape(-1) for p in params])
+        flat = flat.detach()
+        x = x.contiguous()
+        out, saved = stage_forward(x, flat, spec, save=True)
+        ctx.spec = spec
+        ctx.shapes = [p.shape for p in params]
+        ctx.save_for_backward(x, flat, out, saved if saved is not None else torch.empty(0, device=x.device))
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, flat, out, saved = ctx.saved_tensors
+        spec = ctx.spec
+        gin, gp = stage_backward(x, flat, spec, out, saved if saved.numel() else None, grad_out,
+                                 need_grad_in=ctx.needs_input_grad[0])
+        grads, o = [], 0
+        for shp in ctx.shapes:
+            n = 1
+            for s in shp:
+                n *= s
+            grads.append(gp[o:o + n].view(shp))
+            o += n
+        return (gin, None, *grads)
+
+
+def fused_mlp(x: torch.Tensor, spec: MlpSpec, params: list[torch.Tensor]) -> torch.Tensor:
+    if x.is_cuda and nat.native_enabled():
+        if not spec.native_supported():
+            nat.require(x.device)  # raises if the library is missing
+            raise NotImplementedError(f"no fused kernel instantiated for {spec}")
+        return FusedMLPFunction.apply(x, spec, *params)
+    flat = torch.cat([p.reshape(-1) for p in params])
+    return mlp_forward_ref(flat, spec, x)

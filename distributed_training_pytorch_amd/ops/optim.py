@@ -1,0 +1,96 @@
+"""Flat-buffer optimizers (Adam / SGD) over [n_models, P] parameters.
+
+The math is the element-for-element mirror of torch.optim.Adam / SGD
+(``csrc/optim_core.h``); the PyTorch reference below is used on CPU and by the
+numerics tests.  The reference trains with Adam(lr=1e-3) (``demo.py:80-81``).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import _native as nat
+
+
+@dataclass
+class OptimConfig:
+    name: str = "adam"  # "adam" | "sgd"
+    lr: float = 1e-3
+    betas: tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    momentum: float = 0.0
+
+    @property
+    def kind(self) -> int:
+        if self.name == "adam":
+            return nat.MODE_ADAM
+        if self.name == "sgd":
+            return nat.MODE_SGD
+        raise ValueError(f"unknown optimizer {self.name!r}")
+
+    def hyper(self, slope: float = 0.01, grad_scale: float = 1.0) -> nat.Hyper:
+        return nat.Hyper(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.momentum,
+                         slope, grad_scale)
+
+    def torch_optimizer(self, params):
+        if self.name == "adam":
+            return torch.optim.Adam(params, lr=self.lr, betas=self.betas, eps=self.eps,
+                                    weight_decay=self.weight_decay)
+        return torch.optim.SGD(params, lr=self.lr, momentum=self.momentum, weight_decay=self.weight_decay)
+
+
+def adam_update_ref(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tensor, t1: int,
+                    cfg: OptimConfig) -> None:
+    """In-place Adam step number t1 (1-based) with torch's operation order (fp32)."""
+    b1, b2 = cfg.betas
+    if cfg.weight_decay:
+        g = g + cfg.weight_decay * p
+    m.lerp_(g, 1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** t1
+    bc2 = 1 - b2 ** t1
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(cfg.eps)
+    p.addcdiv_(m, denom, value=-(cfg.lr / bc1))
+
+
+def sgd_update_ref(p: torch.Tensor, buf: torch.Tensor, g: torch.Tensor, first: bool, cfg: OptimConfig) -> None:
+    if cfg.weight_decay:
+        g = g + cfg.weight_decay * p
+    if cfg.momentum:
+        if first:
+            buf.copy_(g)
+        else:
+            buf.mul_(cfg.momentum).add_(g)
+        g = buf
+    p.add_(g, alpha=-cfg.lr)
+
+
+def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: float = 1.0,
+                        loss_log=None, loss_scale: float = 1.0, slope: float = 0.01) -> None:
+    """One optimizer step over [n_models, P] flat buffers.
+
+    ``grad`` is [n_models*P (+ n_models losses)] -- the all-reduced comm buffer;
+    ``step`` is the per-model int32 step counter (device or CPU).
+    """
+    n_models, P = params.shape
+    if params.is_cuda and nat.native_enabled():
+        lib = nat.require(params.device)
+        a = nat.OptArgs(nat.ptr(params), nat.ptr(m), nat.ptr(v), nat.ptr(step), nat.ptr(grad),
+                        nat.ptr(loss_log), 0 if loss_log is None else loss_log.shape[0], n_models, P, cfg.kind,
+                        loss_scale, 0, cfg.hyper(slope, grad_scale))
+        nat.check(lib.dtp_flat_optimizer(ctypes.byref(a), nat.stream_ptr()), "dtp_flat_optimizer")
+        return
+    g = grad[: n_models * P].view(n_models, P) * grad_scale
+    for i in range(n_models):
+        t = int(step[i])
+        if cfg.name == "adam":
+            adam_update_ref(params[i], m[i], v[i], g[i], t + 1, cfg)
+        else:
+            sgd_update_ref(params[i], m[i], g[i], t == 0, cfg)
+        if loss_log is not None:
+            loss_log[t % loss_log.shape[0], i] = grad[n_models * P + i] * loss_scale
+        step[i] = t + 1
