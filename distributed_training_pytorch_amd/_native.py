@@ -41,7 +41,7 @@ class SamplerCfg(ctypes.Structure):
         ("batch", c_int),
         ("num_samples", c_int),
         ("steps_per_epoch", c_int),
-        ("half_bits", c_int),
+        ("bits", c_int),
         ("seed", c_uint64),
     ]
 
@@ -133,6 +133,7 @@ def _declare(lib):
         "dtp_mlp_supported": (c_int, [c_int] * 5),
         "dtp_mlp_param_count": (c_int, [c_int] * 4),
         "dtp_mlp_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
+        "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),

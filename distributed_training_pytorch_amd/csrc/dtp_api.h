@@ -51,6 +51,7 @@ const char* dtp_last_error(void);
 int dtp_mlp_supported(int in, int h, int nl, int out, int final_act);
 int dtp_mlp_param_count(int in, int h, int nl, int out);
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream);
+int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream);
 
 // ---- stage forward / backward (autograd path, layer-split pipeline) ----
 struct DtpStageArgs {

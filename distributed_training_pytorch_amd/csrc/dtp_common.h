@@ -54,4 +54,8 @@ DTP_HD double pow_int(double b, uint64_t e) {
   return r;
 }
 
+// error reporting shared by every translation unit (defined in runtime.hip)
+int set_err(int code, const char* msg);
+int check_launch(const char* what);
+
 }  // namespace dtp

@@ -43,7 +43,16 @@ struct Stage {
     return o;
   }
   static constexpr int lb(int l) { return lw(l) + dout(l) * pad4(din(l)); }
-  static constexpr int LP = lw(NL);
+  static constexpr int LPR = lw(NL);
+  // second, transposed copy W^T[in][pad4(out)] for the forward: consecutive
+  // outputs j, j+1 of one input i are adjacent -> v_pk_fma_f32 straight from a
+  // ds_read_b128, no register shuffles (the backward reads the row-major copy)
+  static constexpr int lwt(int l) {
+    int o = LPR;
+    for (int k = 0; k < l; ++k) o += din(k) * pad4(dout(k));
+    return o;
+  }
+  static constexpr int LP = lwt(NL);
   static constexpr int NPT = (P + kBlock - 1) / kBlock;  // params per thread in the optimizer phase
   // saved activations for the stage backward: h_1 .. h_{NL-1} (hidden widths)
   static constexpr int SAVED = (NL - 1) * H;
@@ -67,6 +76,29 @@ DTP_DEV int lds_pos(int p) {
   return r;
 }
 
+// global parameter index -> position in the transposed forward copy (-1 for biases)
+template <class S>
+DTP_DEV int lds_pos_t(int p) {
+  int r = -1;
+  static_for<0, S::NL>([&](auto LC) {
+    constexpr int l = decltype(LC)::value;
+    constexpr int I = S::din(l), O = S::dout(l);
+    if (p >= S::gw(l) && p < S::gb(l)) {
+      const int q = p - S::gw(l);
+      r = S::lwt(l) + (q % I) * S::pad4(O) + (q / I);
+    }
+  });
+  return r;
+}
+
+// stage parameter p (torch order) into both LDS copies
+template <class S>
+DTP_DEV void lds_store_param(float* __restrict__ sw, int p, float v) {
+  sw[lds_pos<S>(p)] = v;
+  const int t = lds_pos_t<S>(p);
+  if (t >= 0) sw[t] = v;
+}
+
 // global parameter index -> (layer, row, col) position in the reduced dW tiles
 template <class S>
 DTP_DEV int tile_pos(int p) {
@@ -84,58 +116,91 @@ DTP_DEV int tile_pos(int p) {
   return r;
 }
 
-// forward of one sample: h[0] is the input, h[l+1] the output of layer l
+// forward of one sample: h[0] is the input, h[l+1] the output of layer l.
+// Each layer first pulls its whole W^T slice out of LDS (broadcast
+// ds_read_b128, all issued back to back so their latency overlaps), then runs
+// the FMA chains (pairs of outputs per v_pk_fma_f32).
 template <class S>
 DTP_DEV void mlp_forward(const float* __restrict__ sw, float (&h)[S::NL + 1][16], float slope) {
   static_for<0, S::NL>([&](auto LC) {
     constexpr int l = decltype(LC)::value;
-    constexpr int I = S::din(l), O = S::dout(l), IP = S::pad4(I);
-    static_for<0, O>([&](auto JC) {
-      constexpr int j = decltype(JC)::value;
-      float z = sw[S::lb(l) + j];
+    constexpr int I = S::din(l), O = S::dout(l), OP = S::pad4(O);
+    float4 wt[I][OP / 4];
+    float4 bb[OP / 4];
+    static_for<0, OP / 4>([&](auto QC) {
+      constexpr int q = decltype(QC)::value;
+      bb[q] = *reinterpret_cast<const float4*>(sw + S::lb(l) + 4 * q);
       static_for<0, I>([&](auto IC) {
         constexpr int i = decltype(IC)::value;
-        z = fmaf(sw[S::lw(l) + j * IP + i], h[l][i], z);
+        wt[i][q] = *reinterpret_cast<const float4*>(sw + S::lwt(l) + i * OP + 4 * q);
       });
+    });
+    float z[OP];
+    static_for<0, OP / 4>([&](auto QC) {
+      constexpr int q = decltype(QC)::value;
+      z[4 * q + 0] = bb[q].x;
+      z[4 * q + 1] = bb[q].y;
+      z[4 * q + 2] = bb[q].z;
+      z[4 * q + 3] = bb[q].w;
+    });
+    static_for<0, I>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      const float hi = h[l][i];
+      static_for<0, OP / 4>([&](auto QC) {
+        constexpr int q = decltype(QC)::value;
+        if constexpr (4 * q + 0 < O) z[4 * q + 0] = fmaf(wt[i][q].x, hi, z[4 * q + 0]);
+        if constexpr (4 * q + 1 < O) z[4 * q + 1] = fmaf(wt[i][q].y, hi, z[4 * q + 1]);
+        if constexpr (4 * q + 2 < O) z[4 * q + 2] = fmaf(wt[i][q].z, hi, z[4 * q + 2]);
+        if constexpr (4 * q + 3 < O) z[4 * q + 3] = fmaf(wt[i][q].w, hi, z[4 * q + 3]);
+      });
+    });
+    static_for<0, O>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
       if constexpr (S::act(l)) {
-        h[l + 1][j] = leaky(z, slope);
+        h[l + 1][j] = leaky(z[j], slope);
       } else {
-        h[l + 1][j] = z;
+        h[l + 1][j] = z[j];
       }
     });
   });
 }
 
-// One wave-local LDS staging area: rows = the wave's 64 samples, 16 floats per
-// row; 16-byte chunks XOR-swizzled by ((row >> 1) & 3) so that both the
-// row-per-lane ds_write_b128 and the MFMA-operand ds_read_b32 pattern are
-// bank-conflict free (8-lane write groups hit 8 distinct 4-bank sets; each
-// 32-lane read half covers banks 0..31 once).
-DTP_DEV int swz(int row, int chunk) { return row * 16 + ((chunk ^ ((row >> 1) & 3)) << 2); }
+// One wave-local LDS staging area per operand (dz rows, h rows): the wave's 64
+// samples s = 4t + q are stored as [q][col][t] (q stride kStgQ = 264 floats), so
+//   * the writer (lane = sample) issues one ds_write_b32 per used column; for a
+//     fixed column the 32 lanes of a half hit 32 distinct banks (264 = 8 mod 32);
+//   * the MFMA reader (lane = (q = l>>4, col = l&15)) finds its 16 K-step operands
+//     contiguous: 4 ds_read_b128, one wait, then 16 back-to-back MFMAs.
+// Unused columns are never written: garbage there only reaches tile rows/cols
+// nobody reads (D[i][j] depends on A row i and B column j only).
+constexpr int kStgQ = 264;
+constexpr int kStgArr = 4 * kStgQ;  // floats per staged operand array
 
 template <int N>
 DTP_DEV void stage_row(float* __restrict__ buf, int lane, const float (&v)[16]) {
+  float* p = buf + (lane & 3) * kStgQ + (lane >> 2);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float4 x;
-    x.x = (4 * c + 0 < N) ? v[4 * c + 0] : 0.f;
-    x.y = (4 * c + 1 < N) ? v[4 * c + 1] : 0.f;
-    x.z = (4 * c + 2 < N) ? v[4 * c + 2] : 0.f;
-    x.w = (4 * c + 3 < N) ? v[4 * c + 3] : 0.f;
-    *reinterpret_cast<float4*>(buf + swz(lane, c)) = x;
-  }
+  for (int c = 0; c < N; ++c) p[c * 16] = v[c];
 }
 
 // acc += sum over the wave's 64 samples of dz[s] (x) h[s]   (16x16 tile)
 DTP_DEV f32x4 wave_outer_acc(const float* __restrict__ dzb, const float* __restrict__ hb, f32x4 acc0, int lane) {
-  const int q = lane >> 4, col = lane & 15, c = col >> 2, w = col & 3;
+  const int off = (lane >> 4) * kStgQ + (lane & 15) * 16;
+  const float4* a4 = reinterpret_cast<const float4*>(dzb + off);
+  const float4* b4 = reinterpret_cast<const float4*>(hb + off);
+  float4 a[4], b[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = a4[i];
+    b[i] = b4[i];
+  }
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int t = 0; t < 16; t += 2) {
-    const int s0 = 4 * t + q, s1 = s0 + 4;
-    const int o0 = swz(s0, c) + w, o1 = swz(s1, c) + w;
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(dzb[o0], hb[o0], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(dzb[o1], hb[o1], acc1, 0, 0, 0);
+  for (int i = 0; i < 4; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[i].x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[i].y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[i].z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[i].w, acc1, 0, 0, 0);
   }
   return acc0 + acc1;
 }
@@ -143,12 +208,15 @@ DTP_DEV f32x4 wave_outer_acc(const float* __restrict__ dzb, const float* __restr
 // Backward of one sample through all layers, starting from dz (gradient w.r.t.
 // the pre-activation output of the LAST layer).  Accumulates the wave's dW tiles
 // into acc[l]; writes d(input) into dx when WANT_DX.
-// stg: this wave's staging area, 2 x 1024 floats (dz rows, then h rows).
-template <class S, bool WANT_DX>
+// stg: this wave's staging area, 2 x kStgArr floats (dz rows, then h rows).
+// LOSS_ROW: dz[OUT] carries the sample's loss value into an otherwise unused
+// row of the output-layer tile; against the constant-1 bias column it sums the
+// batch loss inside the same MFMAs (tile entry (NL-1, OUT, din(NL-1))).
+template <class S, bool WANT_DX, bool LOSS_ROW = false>
 DTP_DEV void mlp_backward(const float* __restrict__ sw, const float (&h)[S::NL + 1][16], float (&dz)[16],
                           float* __restrict__ stg, f32x4 (&acc)[S::NL], float slope, int lane, float (&dx)[16]) {
   float* dzb = stg;
-  float* hb = stg + 1024;
+  float* hb = stg + kStgArr;
   static_for<0, S::NL>([&](auto RC) {
     constexpr int l = S::NL - 1 - decltype(RC)::value;
     constexpr int I = S::din(l), O = S::dout(l), IP = S::pad4(I);
@@ -156,17 +224,34 @@ DTP_DEV void mlp_backward(const float* __restrict__ sw, const float (&h)[S::NL +
     float hr[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) hr[i] = (i < I) ? h[l][i] : (i == I ? 1.f : 0.f);
-    stage_row<O>(dzb, lane, dz);
+    if constexpr (LOSS_ROW && l == S::NL - 1) {
+      static_assert(S::OUT + 1 <= 16, "loss row needs a free tile row");
+      stage_row<O + 1>(dzb, lane, dz);
+    } else {
+      stage_row<O>(dzb, lane, dz);
+    }
     stage_row<I + 1>(hb, lane, hr);
     // input gradient: g = W_l^T dz  (row-major reads of W_l: ds_read_b128 broadcasts)
     if constexpr (l > 0 || WANT_DX) {
-      float g[16];
-      static_for<0, I>([&](auto IC) { g[decltype(IC)::value] = 0.f; });
+      float4 wr[O][IP / 4];
       static_for<0, O>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        static_for<0, I>([&](auto IC) {
-          constexpr int i = decltype(IC)::value;
-          g[i] = fmaf(sw[S::lw(l) + j * IP + i], dz[j], g[i]);
+        static_for<0, IP / 4>([&](auto QC) {
+          constexpr int q = decltype(QC)::value;
+          wr[j][q] = *reinterpret_cast<const float4*>(sw + S::lw(l) + j * IP + 4 * q);
+        });
+      });
+      float g[IP];
+      static_for<0, IP>([&](auto IC) { g[decltype(IC)::value] = 0.f; });
+      static_for<0, O>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float d = dz[j];
+        static_for<0, IP / 4>([&](auto QC) {
+          constexpr int q = decltype(QC)::value;
+          if constexpr (4 * q + 0 < I) g[4 * q + 0] = fmaf(wr[j][q].x, d, g[4 * q + 0]);
+          if constexpr (4 * q + 1 < I) g[4 * q + 1] = fmaf(wr[j][q].y, d, g[4 * q + 1]);
+          if constexpr (4 * q + 2 < I) g[4 * q + 2] = fmaf(wr[j][q].z, d, g[4 * q + 2]);
+          if constexpr (4 * q + 3 < I) g[4 * q + 3] = fmaf(wr[j][q].w, d, g[4 * q + 3]);
         });
       });
       if constexpr (l > 0) {
@@ -195,6 +280,10 @@ DTP_DEV void store_partial_tiles(float* __restrict__ red, const f32x4 (&acc)[S::
     for (int r = 0; r < 4; ++r) t[(4 * q + r) * 16 + col] = acc[l][r];
   }
 }
+
+// tile position of the loss row entry (see mlp_backward LOSS_ROW)
+template <class S>
+constexpr int loss_tile_pos() { return (S::NL - 1) * 256 + S::OUT * 16 + S::din(S::NL - 1); }
 
 template <class S>
 DTP_DEV float sum_partial_tiles(const float* __restrict__ red, int tpos, int nwaves) {

@@ -1,0 +1,175 @@
+// Layer-split stage kernels (autograd path): forward one lane per sample,
+// backward = input-gradient VALU chain + MFMA weight-gradient reduction
+// (mlp_core.h).  Equivalent of one MultiGPUModel stage of
+// demo_one_model_multi_gpu.py:17-42 and of nn.Sequential fwd/bwd in
+// toy_model_and_data.py:8-25.
+#include <string>
+
+#include "dtp_api.h"
+#include "mlp_core.h"
+
+namespace dtp {
+constexpr int kStage = 2 * kStgArr;
+
+// stage forward: one lane per sample, any number of workgroups
+template <class S>
+__global__ __launch_bounds__(kBlock) void mlp_stage_fwd_kernel(DtpStageArgs a) {
+  __shared__ __align__(16) float sw[S::pad4(S::LP)];
+  for (int p = threadIdx.x; p < S::P; p += kBlock) lds_store_param<S>(sw, p, a.params[p]);
+  __syncthreads();
+  const int b = blockIdx.x * kBlock + threadIdx.x;
+  if (b >= a.batch) return;
+  float h[S::NL + 1][16];
+  static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = a.x[(size_t)b * S::IN + decltype(IC)::value]; });
+  mlp_forward<S>(sw, h, a.slope);
+  static_for<0, S::OUT>([&](auto JC) { a.out[(size_t)b * S::OUT + decltype(JC)::value] = h[S::NL][decltype(JC)::value]; });
+  if (a.saved) {
+    static_for<1, S::NL>([&](auto LC) {
+      constexpr int l = decltype(LC)::value;
+      static_for<0, S::H>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        a.saved[(size_t)b * S::SAVED + (l - 1) * S::H + i] = h[l][i];
+      });
+    });
+  }
+}
+
+// stage backward: grid-stride over 256-sample chunks; per-wave MFMA dW tiles,
+// LDS reduction, then one plain store (single block) or float atomics (multi block)
+template <class S, bool WANT_DX>
+__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
+  __shared__ __align__(16) struct {
+    float w[S::pad4(S::LP)];
+    float stage[4][kStage];
+  } sm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int p = tid; p < S::P; p += kBlock) lds_store_param<S>(sm.w, p, a.params[p]);
+  __syncthreads();
+  f32x4 acc[S::NL];
+#pragma unroll
+  for (int l = 0; l < S::NL; ++l) acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = blockIdx.x * kBlock; c0 < a.batch; c0 += gridDim.x * kBlock) {
+    const int b = c0 + tid;
+    const bool valid = b < a.batch;
+    float h[S::NL + 1][16];
+    static_for<0, S::IN>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      h[0][i] = valid ? a.x[(size_t)b * S::IN + i] : 0.f;
+    });
+    static_for<1, S::NL>([&](auto LC) {
+      constexpr int l = decltype(LC)::value;
+      static_for<0, S::H>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        h[l][i] = valid ? a.saved[(size_t)b * S::SAVED + (l - 1) * S::H + i] : 0.f;
+      });
+    });
+    float dz[16];
+    static_for<0, S::OUT>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      float go = valid ? a.grad_out[(size_t)b * S::OUT + j] : 0.f;
+      if constexpr (S::FINAL_ACT) go *= leaky_grad_from_out(valid ? a.out[(size_t)b * S::OUT + j] : 0.f, a.slope);
+      dz[j] = go;
+    });
+    float dx[16];
+    mlp_backward<S, WANT_DX>(sm.w, h, dz, &sm.stage[wave][0], acc, a.slope, lane, dx);
+    if constexpr (WANT_DX) {
+      if (valid) {
+        static_for<0, S::IN>([&](auto IC) {
+          a.grad_in[(size_t)b * S::IN + decltype(IC)::value] = dx[decltype(IC)::value];
+        });
+      }
+    }
+  }
+  __syncthreads();
+  store_partial_tiles<S>(&sm.stage[0][0], acc, wave, lane);
+  __syncthreads();
+  for (int p = tid; p < S::P; p += kBlock) {
+    const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
+    if (gridDim.x == 1)
+      a.grad_params[p] = g;
+    else
+      atomicAdd(&a.grad_params[p], g);
+  }
+}
+
+}  // namespace dtp
+
+namespace {
+using dtp::check_launch;
+using dtp::set_err;
+
+// (IN, H, NL, OUT, FINAL_ACT): every contiguous layer range of the toy model
+// (layer-split stages) plus the train shapes as whole-model stages
+#define DTP_STAGE_SHAPES(X) \
+  X(2, 10, 5, 1, false)     \
+  X(2, 10, 4, 10, true)     \
+  X(10, 10, 4, 1, false)    \
+  X(2, 10, 3, 10, true)     \
+  X(10, 10, 3, 10, true)    \
+  X(10, 10, 3, 1, false)    \
+  X(2, 10, 2, 10, true)     \
+  X(10, 10, 2, 10, true)    \
+  X(10, 10, 2, 1, false)    \
+  X(2, 10, 1, 10, true)     \
+  X(10, 10, 1, 10, true)    \
+  X(10, 10, 1, 1, false)    \
+  X(2, 10, 3, 1, false)     \
+  X(2, 10, 5, 2, false)     \
+  X(2, 10, 5, 4, false)     \
+  X(2, 15, 5, 1, false)     \
+  X(2, 15, 5, 4, false)     \
+  X(4, 15, 5, 4, false)
+
+template <class S>
+int launch_stage_fwd(const DtpStageArgs* a, hipStream_t st) {
+  if (a->batch <= 0) return 0;
+  dim3 grid((a->batch + dtp::kBlock - 1) / dtp::kBlock), block(dtp::kBlock);
+  hipLaunchKernelGGL((dtp::mlp_stage_fwd_kernel<S>), grid, block, 0, st, *a);
+  return check_launch("mlp_stage_fwd_kernel");
+}
+
+template <class S>
+int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
+  if (a->batch <= 0) return 0;
+  // one block reduces deterministically up to 4 chunks; larger batches spread
+  // over more CUs and combine with float atomics into the zeroed grad buffer
+  int nblk = (a->batch + 4 * dtp::kBlock - 1) / (4 * dtp::kBlock);
+  if (nblk > 256) nblk = 256;
+  dim3 grid(nblk), block(dtp::kBlock);
+  if (a->grad_in)
+    hipLaunchKernelGGL((dtp::mlp_stage_bwd_kernel<S, true>), grid, block, 0, st, *a);
+  else
+    hipLaunchKernelGGL((dtp::mlp_stage_bwd_kernel<S, false>), grid, block, 0, st, *a);
+  return check_launch("mlp_stage_bwd_kernel");
+}
+}  // namespace
+
+extern "C" {
+
+int dtp_mlp_supported(int in, int h, int nl, int out, int final_act) {
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return 1;
+  DTP_STAGE_SHAPES(X)
+#undef X
+  return 0;
+}
+
+int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_fwd<dtp::Stage<I, H, N, O, F>>(a, st);
+  DTP_STAGE_SHAPES(X)
+#undef X
+  return set_err(-2, "mlp stage shape not instantiated");
+}
+
+int dtp_mlp_stage_bwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd<dtp::Stage<I, H, N, O, F>>(a, st);
+  DTP_STAGE_SHAPES(X)
+#undef X
+  return set_err(-2, "mlp stage shape not instantiated");
+}
+
+}  // extern "C"

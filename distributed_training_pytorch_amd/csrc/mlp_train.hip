@@ -20,18 +20,37 @@
 namespace dtp {
 
 constexpr int kDataCache = 4096;  // floats of dataset that may be staged in LDS
+constexpr int kPermCap = 2048;    // per-rank epoch permutation kept in LDS
+constexpr int kStage = 2 * kStgArr;
 
 template <class S>
 struct TrainSmem {
   float w[S::pad4(S::LP)];
-  float stage[4][2048];  // per wave: 64 dz rows + 64 h rows; reused for the dW tile reduction
+  float stage[4][kStage];  // per wave: dz rows + h rows; reused for the dW tile reduction
   float data[kDataCache];
-  float lred[4];
+  int perm[kPermCap];
 };
 
-template <class S, int MODE>
-__global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
-  static_assert(4 * S::NL * 256 <= 4 * 2048, "reduction tiles must fit in the staging area");
+// In-kernel phase stamps (diagnostic instantiation only, PROF = true): thread 0
+// records s_memtime at phase boundaries of the first 8 iterations;
+// per-wave end-of-backward stamps at [8 + wave].  Never used on timed runs.
+#define DTP_STAMP(K)                                                                     \
+  do {                                                                                   \
+    if constexpr (PROF) {                                                                \
+      if (lane == 0 && it < 8 && ((K) >= 8 || wave == 0)) {                              \
+        unsigned long long _t;                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");       \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        prof[((size_t)blockIdx.x * 8 + it) * 16 + (K)] = _t;                             \
+      }                                                                                  \
+    }                                                                                    \
+  } while (0)
+
+template <class S, int MODE, bool PROF = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void mlp_train_kernel(
+    DtpTrainArgs a) {
+  static_assert(4 * S::NL * 256 <= 4 * kStage, "reduction tiles must fit in the staging area");
   __shared__ __align__(16) TrainSmem<S> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
@@ -39,28 +58,33 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   constexpr bool kUpdate = MODE != DTP_MODE_GRAD;
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
+  unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
   const bool ce = a.loss == DTP_LOSS_CE;
   const int ydim = ce ? 1 : S::OUT;
 
   float* __restrict__ gp = a.params + (size_t)model * P;
-  for (int p = tid; p < P; p += kBlock) sm.w[lds_pos<S>(p)] = gp[p];
+  for (int p = tid; p < P; p += kBlock) lds_store_param<S>(sm.w, p, gp[p]);
 
-  const int rowf = S::IN + ydim;
-  const bool cached = a.cache_data && a.smp.n * rowf <= kDataCache;
+  const SamplerCfg smp = a.smp;
+  const bool cached = a.cache_data && smp.n * (S::IN + ydim) <= kDataCache;
   if (cached) {
-    for (int e = tid; e < a.smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
-    for (int e = tid; e < a.smp.n * ydim; e += kBlock) sm.data[a.smp.n * S::IN + e] = a.Y[e];
+    for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
+    for (int e = tid; e < smp.n * ydim; e += kBlock) sm.data[smp.n * S::IN + e] = a.Y[e];
   }
-  const float* __restrict__ Xs = cached ? sm.data : a.X;
-  const float* __restrict__ Ys = cached ? sm.data + a.smp.n * S::IN : a.Y;
+  // (two explicit paths: a select between an LDS and a global pointer would
+  // degrade every sample load to a flat_load)
+  const float* __restrict__ Xg = a.X;
+  const float* __restrict__ Yg = a.Y;
+  const int yoff = smp.n * S::IN;
 
   // this thread owns parameters tid, tid+256, ... in the optimizer phase
-  int lp[S::NPT], tp[S::NPT];
+  int lp[S::NPT], lpt[S::NPT], tp[S::NPT];
   float mr[S::NPT], vr[S::NPT];
 #pragma unroll
   for (int k = 0; k < S::NPT; ++k) {
     const int p = tid + k * kBlock;
     lp[k] = lds_pos<S>(p < P ? p : 0);
+    lpt[k] = lds_pos_t<S>(p < P ? p : 0);
     tp[k] = tile_pos<S>(p < P ? p : 0);
     mr[k] = 0.f;
     vr[k] = 0.f;
@@ -69,51 +93,86 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       if (kAdam) vr[k] = a.opt_v[(size_t)model * P + p];
     }
   }
-  const long long t0 = a.step[model];
+  // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
+  const int t0 = a.step[model];
+  const bool explicit_idx = smp.mode == SAMPLER_EXPLICIT;
+  int epoch = explicit_idx ? 0 : t0 / smp.steps_per_epoch;
+  int bi = explicit_idx ? 0 : t0 - epoch * smp.steps_per_epoch;
+  int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
+  uint32_t keys[4];
+  epoch_keys(smp, epoch, keys);
+  // the shuffled epoch order is computed once per epoch into LDS (cooperatively),
+  // so a step's gather is one LDS read per sample
+  const bool use_perm = smp.mode == SAMPLER_DIST_SHUFFLE && smp.num_samples <= kPermCap;
+  auto fill_perm = [&](int ep) {
+    uint32_t kk[4];
+    epoch_keys(smp, ep, kk);
+    const BatchPos b0{ep, 0, 0};
+    for (int pos = tid; pos < smp.num_samples; pos += kBlock) sm.perm[pos] = sample_index(smp, b0, kk, pos);
+  };
+  if (use_perm) fill_perm(epoch);
+  // Adam bias-correction powers beta^t, carried in double like torch's host math
+  double b1t = kAdam ? pow_int(a.hp.beta1, (uint64_t)t0) : 1.0;
+  double b2t = kAdam ? pow_int(a.hp.beta2, (uint64_t)t0) : 1.0;
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
   __syncthreads();
 
   for (int it = 0; it < a.n_steps; ++it) {
-    const long long t = t0 + it;
-    int bsz;
-    BatchPos bp{};
-    uint32_t keys[4] = {0u, 0u, 0u, 0u};
-    const bool explicit_idx = a.smp.mode == SAMPLER_EXPLICIT;
-    if (explicit_idx) {
-      bsz = a.smp.batch;
-    } else {
-      bp = batch_pos(a.smp, t);
-      epoch_keys(a.smp, bp.epoch, keys);
-      bsz = bp.size;
-    }
+    DTP_STAMP(0);
+    const int t = t0 + it;
+    BatchPos bp;
+    bp.epoch = epoch;
+    bp.start = bi * smp.batch;
+    bp.size = explicit_idx ? smp.batch : min(smp.batch, smp.num_samples - bp.start);
+    const int bsz = bp.size;
     const float inv = ce ? 1.f / (float)bsz : 1.f / (float)(bsz * S::OUT);
 
     f32x4 acc[S::NL];
 #pragma unroll
     for (int l = 0; l < S::NL; ++l) acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float lsum = 0.f;
 
     for (int c0 = 0; c0 < bsz; c0 += kBlock) {
       const int k = c0 + tid;
       const bool valid = k < bsz;
       int di = 0;
-      if (valid) di = explicit_idx ? a.idx[(size_t)it * a.smp.batch + k] : sample_index(a.smp, bp, keys, k);
+      if (valid)
+        di = explicit_idx ? a.idx[(size_t)it * smp.batch + k]
+                          : (use_perm ? sm.perm[bp.start + k] : sample_index(smp, bp, keys, k));
       float h[S::NL + 1][16];
-      static_for<0, S::IN>([&](auto IC) {
-        constexpr int i = decltype(IC)::value;
-        h[0][i] = valid ? Xs[(size_t)di * S::IN + i] : 0.f;
-      });
+      float yv[16];
+      if (cached) {
+        static_for<0, S::IN>([&](auto IC) {
+          constexpr int i = decltype(IC)::value;
+          h[0][i] = valid ? sm.data[di * S::IN + i] : 0.f;
+        });
+        static_for<0, S::OUT>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;
+          yv[j] = (valid && (j < ydim)) ? sm.data[yoff + di * ydim + j] : 0.f;
+        });
+      } else {
+        static_for<0, S::IN>([&](auto IC) {
+          constexpr int i = decltype(IC)::value;
+          h[0][i] = valid ? Xg[(size_t)di * S::IN + i] : 0.f;
+        });
+        static_for<0, S::OUT>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;
+          yv[j] = (valid && (j < ydim)) ? Yg[(size_t)di * ydim + j] : 0.f;
+        });
+      }
+      if (c0 == 0) DTP_STAMP(1);
       mlp_forward<S>(sm.w, h, a.hp.slope);
       float dz[16];
       if (!ce) {
+        float l2 = 0.f;
         static_for<0, S::OUT>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
-          const float d = h[S::NL][j] - (valid ? Ys[(size_t)di * S::OUT + j] : 0.f);
-          lsum += valid ? d * d : 0.f;
+          const float d = h[S::NL][j] - yv[j];
+          l2 += d * d;
           dz[j] = valid ? 2.f * d * inv : 0.f;
         });
+        dz[S::OUT] = valid ? l2 : 0.f;  // loss row
       } else {
-        const int cls = valid ? (int)Ys[di] : 0;
+        const int cls = (int)yv[0];
         float mx = h[S::NL][0];
         static_for<1, S::OUT>([&](auto JC) { mx = fmaxf(mx, h[S::NL][decltype(JC)::value]); });
         float se = 0.f, zc = 0.f;
@@ -124,27 +183,30 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
           zc = (j == cls) ? h[S::NL][j] : zc;
         });
         const float lse = mx + __logf(se);
-        lsum += valid ? lse - zc : 0.f;
         const float rs = 1.f / se;
         static_for<0, S::OUT>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
           dz[j] = valid ? (dz[j] * rs - (j == cls ? 1.f : 0.f)) * inv : 0.f;
         });
+        dz[S::OUT] = valid ? lse - zc : 0.f;  // loss row
       }
+      if (c0 == 0) DTP_STAMP(2);
       float dx[16];
-      mlp_backward<S, false>(sm.w, h, dz, &sm.stage[wave][0], acc, a.hp.slope, lane, dx);
+      mlp_backward<S, false, true>(sm.w, h, dz, &sm.stage[wave][0], acc, a.hp.slope, lane, dx);
     }
-
-    lsum = wave_sum(lsum);
+    DTP_STAMP(8 + wave);
+    DTP_STAMP(3);
     __syncthreads();  // every wave is done with its staging rows
     store_partial_tiles<S>(&sm.stage[0][0], acc, wave, lane);
-    if (lane == 0) sm.lred[wave] = lsum;
     __syncthreads();
-    const float mean_loss = (sm.lred[0] + sm.lred[1] + sm.lred[2] + sm.lred[3]) * (ce ? inv : inv);
+    DTP_STAMP(4);
 
     float g[S::NPT];
 #pragma unroll
     for (int k = 0; k < S::NPT; ++k) g[k] = sum_partial_tiles<S>(&sm.stage[0][0], tp[k], 4);
+    // sum of per-sample losses rode the output tile's loss row
+    const float mean_loss = sum_partial_tiles<S>(&sm.stage[0][0], loss_tile_pos<S>(), 4) * inv;
+    DTP_STAMP(5);
 
     float gloss = mean_loss;
     if constexpr (kXgmi) {
@@ -156,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
 
     if (tid == 0 && a.loss_log) {
       const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
-      a.loss_log[(size_t)(t % a.loss_log_cap) * a.n_models + model] = lg;
+      a.loss_log[(size_t)lslot * a.n_models + model] = lg;
     }
 
     if constexpr (MODE == DTP_MODE_GRAD) {
@@ -167,7 +229,9 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       }
       if (tid == 0) a.grad_out[(size_t)a.n_models * P + model] = mean_loss;
     } else if constexpr (kAdam) {
-      const AdamScalars s = adam_scalars(a.hp, t + 1);
+      b1t *= a.hp.beta1;
+      b2t *= a.hp.beta2;
+      AdamScalars s = adam_scalars_from_pow(a.hp, b1t, b2t);
 #pragma unroll
       for (int k = 0; k < S::NPT; ++k) {
         const int p = tid + k * kBlock;
@@ -175,6 +239,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
           float w = sm.w[lp[k]];
           adam_update(w, mr[k], vr[k], g[k] * a.hp.grad_scale, s);
           sm.w[lp[k]] = w;
+          if (lpt[k] >= 0) sm.w[lpt[k]] = w;
         }
       }
     } else {
@@ -186,10 +251,21 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
           float w = sm.w[lp[k]];
           sgd_update(w, mr[k], g[k] * a.hp.grad_scale, lr, mom, wd, t == 0);
           sm.w[lp[k]] = w;
+          if (lpt[k] >= 0) sm.w[lpt[k]] = w;
         }
       }
     }
+    DTP_STAMP(6);
+    // advance the sampler / loss-ring position
+    if (!explicit_idx && ++bi == smp.steps_per_epoch) {
+      bi = 0;
+      ++epoch;
+      epoch_keys(smp, epoch, keys);
+      if (use_perm && it + 1 < a.n_steps) fill_perm(epoch);  // ordered by the barrier below
+    }
+    if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
     __syncthreads();  // updated weights visible; reduction tiles consumed
+    DTP_STAMP(7);
   }
 
   if constexpr (kUpdate) {
@@ -202,90 +278,8 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
         if (kAdam) a.opt_v[(size_t)model * P + p] = vr[k];
       }
     }
-    if (tid == 0) a.step[model] = (int)(t0 + a.n_steps);
+    if (tid == 0) a.step[model] = t0 + a.n_steps;
     if (kXgmi && tid == 0) a.epoch[model] = xepoch;
-  }
-}
-
-// ------------------------------------------------------------------------------
-// stage forward: one lane per sample, any number of workgroups
-template <class S>
-__global__ __launch_bounds__(kBlock) void mlp_stage_fwd_kernel(DtpStageArgs a) {
-  __shared__ __align__(16) float sw[S::pad4(S::LP)];
-  for (int p = threadIdx.x; p < S::P; p += kBlock) sw[lds_pos<S>(p)] = a.params[p];
-  __syncthreads();
-  const int b = blockIdx.x * kBlock + threadIdx.x;
-  if (b >= a.batch) return;
-  float h[S::NL + 1][16];
-  static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = a.x[(size_t)b * S::IN + decltype(IC)::value]; });
-  mlp_forward<S>(sw, h, a.slope);
-  static_for<0, S::OUT>([&](auto JC) { a.out[(size_t)b * S::OUT + decltype(JC)::value] = h[S::NL][decltype(JC)::value]; });
-  if (a.saved) {
-    static_for<1, S::NL>([&](auto LC) {
-      constexpr int l = decltype(LC)::value;
-      static_for<0, S::H>([&](auto IC) {
-        constexpr int i = decltype(IC)::value;
-        a.saved[(size_t)b * S::SAVED + (l - 1) * S::H + i] = h[l][i];
-      });
-    });
-  }
-}
-
-// stage backward: grid-stride over 256-sample chunks; per-wave MFMA dW tiles,
-// LDS reduction, then one plain store (single block) or float atomics (multi block)
-template <class S, bool WANT_DX>
-__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
-  __shared__ __align__(16) struct {
-    float w[S::pad4(S::LP)];
-    float stage[4][2048];
-  } sm;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int p = tid; p < S::P; p += kBlock) sm.w[lds_pos<S>(p)] = a.params[p];
-  __syncthreads();
-  f32x4 acc[S::NL];
-#pragma unroll
-  for (int l = 0; l < S::NL; ++l) acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c0 = blockIdx.x * kBlock; c0 < a.batch; c0 += gridDim.x * kBlock) {
-    const int b = c0 + tid;
-    const bool valid = b < a.batch;
-    float h[S::NL + 1][16];
-    static_for<0, S::IN>([&](auto IC) {
-      constexpr int i = decltype(IC)::value;
-      h[0][i] = valid ? a.x[(size_t)b * S::IN + i] : 0.f;
-    });
-    static_for<1, S::NL>([&](auto LC) {
-      constexpr int l = decltype(LC)::value;
-      static_for<0, S::H>([&](auto IC) {
-        constexpr int i = decltype(IC)::value;
-        h[l][i] = valid ? a.saved[(size_t)b * S::SAVED + (l - 1) * S::H + i] : 0.f;
-      });
-    });
-    float dz[16];
-    static_for<0, S::OUT>([&](auto JC) {
-      constexpr int j = decltype(JC)::value;
-      float go = valid ? a.grad_out[(size_t)b * S::OUT + j] : 0.f;
-      if constexpr (S::FINAL_ACT) go *= leaky_grad_from_out(valid ? a.out[(size_t)b * S::OUT + j] : 0.f, a.slope);
-      dz[j] = go;
-    });
-    float dx[16];
-    mlp_backward<S, WANT_DX>(sm.w, h, dz, &sm.stage[wave][0], acc, a.slope, lane, dx);
-    if constexpr (WANT_DX) {
-      if (valid) {
-        static_for<0, S::IN>([&](auto IC) {
-          a.grad_in[(size_t)b * S::IN + decltype(IC)::value] = dx[decltype(IC)::value];
-        });
-      }
-    }
-  }
-  __syncthreads();
-  store_partial_tiles<S>(&sm.stage[0][0], acc, wave, lane);
-  __syncthreads();
-  for (int p = tid; p < S::P; p += kBlock) {
-    const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
-    if (gridDim.x == 1)
-      a.grad_params[p] = g;
-    else
-      atomicAdd(&a.grad_params[p], g);
   }
 }
 
@@ -305,16 +299,8 @@ __global__ void sampler_probe_kernel(SamplerCfg s, long long t0, int n_steps, in
 // ------------------------------------------------------------------------------
 // dispatch tables
 namespace {
-thread_local std::string g_err;
-int set_err(int code, const std::string& m) {
-  g_err = m;
-  return code;
-}
-int check_launch(const char* what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return set_err(-3, std::string(what) + ": " + hipGetErrorString(e));
-  return 0;
-}
+using dtp::check_launch;
+using dtp::set_err;
 
 // (IN, H, NL, OUT): shapes the fused train-step kernel is instantiated for
 #define DTP_TRAIN_SHAPES(X) \
@@ -325,28 +311,6 @@ int check_launch(const char* what) {
   X(2, 15, 5, 1)            \
   X(2, 15, 5, 4)            \
   X(4, 15, 5, 4)
-
-// (IN, H, NL, OUT, FINAL_ACT): every contiguous layer range of the toy model
-// (layer-split stages) plus the train shapes as whole-model stages
-#define DTP_STAGE_SHAPES(X) \
-  X(2, 10, 5, 1, false)     \
-  X(2, 10, 4, 10, true)     \
-  X(10, 10, 4, 1, false)    \
-  X(2, 10, 3, 10, true)     \
-  X(10, 10, 3, 10, true)    \
-  X(10, 10, 3, 1, false)    \
-  X(2, 10, 2, 10, true)     \
-  X(10, 10, 2, 10, true)    \
-  X(10, 10, 2, 1, false)    \
-  X(2, 10, 1, 10, true)     \
-  X(10, 10, 1, 10, true)    \
-  X(10, 10, 1, 1, false)    \
-  X(2, 10, 3, 1, false)     \
-  X(2, 10, 5, 2, false)     \
-  X(2, 10, 5, 4, false)     \
-  X(2, 15, 5, 1, false)     \
-  X(2, 15, 5, 4, false)     \
-  X(4, 15, 5, 4, false)
 
 template <class S>
 int launch_train(const DtpTrainArgs* a, int mode, hipStream_t st) {
@@ -375,41 +339,15 @@ int launch_train(const DtpTrainArgs* a, int mode, hipStream_t st) {
 }
 
 template <class S>
-int launch_stage_fwd(const DtpStageArgs* a, hipStream_t st) {
-  if (a->batch <= 0) return 0;
-  dim3 grid((a->batch + dtp::kBlock - 1) / dtp::kBlock), block(dtp::kBlock);
-  hipLaunchKernelGGL((dtp::mlp_stage_fwd_kernel<S>), grid, block, 0, st, *a);
-  return check_launch("mlp_stage_fwd_kernel");
+int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_ADAM, true>), dim3(a->n_models), dim3(dtp::kBlock), 0, st, *a);
+  return check_launch("mlp_train_kernel<prof>");
 }
 
-template <class S>
-int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
-  if (a->batch <= 0) return 0;
-  // one block reduces deterministically up to 4 chunks; larger batches spread
-  // over more CUs and combine with float atomics into the zeroed grad buffer
-  int nblk = (a->batch + 4 * dtp::kBlock - 1) / (4 * dtp::kBlock);
-  if (nblk > 256) nblk = 256;
-  dim3 grid(nblk), block(dtp::kBlock);
-  if (a->grad_in)
-    hipLaunchKernelGGL((dtp::mlp_stage_bwd_kernel<S, true>), grid, block, 0, st, *a);
-  else
-    hipLaunchKernelGGL((dtp::mlp_stage_bwd_kernel<S, false>), grid, block, 0, st, *a);
-  return check_launch("mlp_stage_bwd_kernel");
-}
 }  // namespace
 
 extern "C" {
 
-int dtp_version(void) { return 1; }
-const char* dtp_last_error(void) { return g_err.c_str(); }
-
-int dtp_mlp_supported(int in, int h, int nl, int out, int final_act) {
-#define X(I, H, N, O, F) \
-  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return 1;
-  DTP_STAGE_SHAPES(X)
-#undef X
-  return 0;
-}
 
 int dtp_mlp_param_count(int in, int h, int nl, int out) {
   int p = 0;
@@ -435,22 +373,9 @@ int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mod
   return set_err(-2, "mlp shape not instantiated for the fused train kernel");
 }
 
-int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-#define X(I, H, N, O, F) \
-  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_fwd<dtp::Stage<I, H, N, O, F>>(a, st);
-  DTP_STAGE_SHAPES(X)
-#undef X
-  return set_err(-2, "mlp stage shape not instantiated");
-}
-
-int dtp_mlp_stage_bwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-#define X(I, H, N, O, F) \
-  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd<dtp::Stage<I, H, N, O, F>>(a, st);
-  DTP_STAGE_SHAPES(X)
-#undef X
-  return set_err(-2, "mlp stage shape not instantiated");
+// diagnostic: toy shape, Adam, phase stamps into a->status (as u64[n_models][8][16])
+int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream) {
+  return launch_train_profile<dtp::Stage<2, 10, 5, 1, false>>(a, (hipStream_t)stream);
 }
 
 int dtp_sampler_indices(const dtp::SamplerCfg* s, long long t0, int n_steps, int* out, void* stream) {

@@ -29,6 +29,20 @@ DTP_DEV AdamScalars adam_scalars(const DtpHyper& hp, long long t1) {
   return s;
 }
 
+// same, from carried powers b1t = beta1^t, b2t = beta2^t (t = the new step number)
+DTP_DEV AdamScalars adam_scalars_from_pow(const DtpHyper& hp, double b1t, double b2t) {
+  AdamScalars s;
+  const double bc1 = 1.0 - b1t, bc2 = 1.0 - b2t;
+  s.step_size = (float)(hp.lr / bc1);
+  s.bc2_sqrt = (float)sqrt(bc2);
+  s.one_m_b1 = (float)(1.0 - hp.beta1);
+  s.b2 = (float)hp.beta2;
+  s.one_m_b2 = (float)(1.0 - hp.beta2);
+  s.eps = (float)hp.eps;
+  s.wd = (float)hp.weight_decay;
+  return s;
+}
+
 DTP_DEV void adam_update(float& p, float& m, float& v, float g, const AdamScalars& s) {
   if (s.wd != 0.f) g = g + s.wd * p;
   m = m + s.one_m_b1 * (g - m);

@@ -31,8 +31,25 @@ struct GraphHandle {
 };
 }  // namespace
 
+namespace dtp {
+int set_err(int code, const char* msg) {
+  g_rt_err = msg;
+  return code;
+}
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_rt_err = std::string(what) + ": " + hipGetErrorString(e);
+    return -3;
+  }
+  return 0;
+}
+}  // namespace dtp
+
 extern "C" {
 
+int dtp_version(void) { return 1; }
+const char* dtp_last_error(void) { return g_rt_err.c_str(); }
 const char* dtp_runtime_last_error(void) { return g_rt_err.c_str(); }
 
 int dtp_get_device(int* dev) {

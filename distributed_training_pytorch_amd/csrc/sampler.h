@@ -33,7 +33,7 @@ struct SamplerCfg {
   int batch;        // per-rank batch size
   int num_samples;  // per-rank samples per epoch
   int steps_per_epoch;
-  int half_bits;    // Feistel half width
+  int bits;         // Feistel domain = 2^bits >= n
   uint64_t seed;
 };
 
@@ -51,18 +51,20 @@ DTP_HD uint32_t round_key(uint64_t seed, uint32_t epoch, uint32_t r) {
   return hash32(lo ^ hash32(hi + epoch * 0x9E3779B9U + r * 0x85EBCA6BU));
 }
 
-DTP_HD uint32_t feistel_permute(uint32_t q, uint32_t n, int half_bits, const uint32_t (&k)[4]) {
-  const uint32_t mask = (1u << half_bits) - 1u;
+// Bijection on [0, 2^bits): 4 rounds of  lo ^= F(hi, key) ; rotate (lo to the
+// top).  Works for any bits (no even-width restriction), so a power-of-two n
+// needs no cycle-walking at all; other n cycle-walk into [0, n).
+DTP_HD uint32_t feistel_permute(uint32_t q, uint32_t n, int bits, const uint32_t (&k)[4]) {
+  const int r = bits > 1 ? (bits >> 1) : 1;
+  const uint32_t rmask = (1u << r) - 1u;
+  const uint32_t dmask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
   do {
-    uint32_t L = q >> half_bits, R = q & mask;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t F = hash32(R ^ k[r]) & mask;
-      const uint32_t nl = R;
-      R = L ^ F;
-      L = nl;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t hi = q >> r;
+      const uint32_t lo = (q & rmask) ^ (hash32(hi ^ k[i]) & rmask);
+      q = ((lo << (bits - r)) | hi) & dmask;
     }
-    q = (L << half_bits) | R;
   } while (q >= n);
   return q;
 }
@@ -88,10 +90,10 @@ DTP_HD BatchPos batch_pos(const SamplerCfg& s, long long t) {
 DTP_HD int sample_index(const SamplerCfg& s, const BatchPos& bp, const uint32_t (&keys)[4], int k) {
   const int pos = bp.start + k;
   if (s.mode == SAMPLER_SEQUENTIAL) return pos;
-  long long q = (long long)s.rank + (long long)pos * s.world;  // position in the padded list
-  q %= s.n;                                                    // padding repeats from the start
-  if (s.mode == SAMPLER_DIST_SHUFFLE) return (int)feistel_permute((uint32_t)q, (uint32_t)s.n, s.half_bits, keys);
-  return (int)q;
+  int q = s.rank + pos * s.world;  // position in the padded list
+  if (q >= s.n) q %= s.n;           // padding repeats from the start
+  if (s.mode == SAMPLER_DIST_SHUFFLE) return (int)feistel_permute((uint32_t)q, (uint32_t)s.n, s.bits, keys);
+  return q;
 }
 
 DTP_HD void epoch_keys(const SamplerCfg& s, int epoch, uint32_t (&k)[4]) {

@@ -47,21 +47,22 @@ def epoch_keys(seed: int, epoch: int) -> list[int]:
     return [round_key(seed, epoch, r) for r in range(4)]
 
 
-def feistel_permute(q: int, n: int, half_bits: int, keys: list[int]) -> int:
-    mask = (1 << half_bits) - 1
+def feistel_permute(q: int, n: int, bits: int, keys: list[int]) -> int:
+    """Bijection on [0, 2**bits) (4 rounds of lo ^= F(hi); rotate), cycle-walked into [0, n)."""
+    r = bits >> 1 if bits > 1 else 1
+    rmask = (1 << r) - 1
+    dmask = (1 << bits) - 1
     while True:
-        L, R = q >> half_bits, q & mask
-        for r in range(4):
-            F = hash32(R ^ keys[r]) & mask
-            L, R = R, L ^ F
-        q = (L << half_bits) | R
+        for i in range(4):
+            hi = q >> r
+            lo = (q & rmask) ^ (hash32(hi ^ keys[i]) & rmask)
+            q = ((lo << (bits - r)) | hi) & dmask
         if q < n:
             return q
 
 
-def half_bits_for(n: int) -> int:
-    bits = max(2, math.ceil(math.log2(max(n, 2))))
-    return (bits + 1) // 2
+def bits_for(n: int) -> int:
+    return max(1, math.ceil(math.log2(max(n, 2))))
 
 
 @dataclass
@@ -93,8 +94,8 @@ class SamplerGeometry:
         return math.ceil(self.num_samples / self.batch)
 
     @property
-    def half_bits(self) -> int:
-        return half_bits_for(self.n)
+    def bits(self) -> int:
+        return bits_for(self.n)
 
     def batch_pos(self, t: int) -> tuple[int, int, int]:
         epoch, bi = divmod(t, self.steps_per_epoch)
@@ -113,14 +114,14 @@ class SamplerGeometry:
         out = []
         for k in range(size):
             q = (self.rank + (start + k) * self.world) % self.n
-            out.append(feistel_permute(q, self.n, self.half_bits, keys) if self.mode == SAMPLER_DIST_SHUFFLE else q)
+            out.append(feistel_permute(q, self.n, self.bits, keys) if self.mode == SAMPLER_DIST_SHUFFLE else q)
         return out
 
     def to_native(self):
         from .._native import SamplerCfg
 
         return SamplerCfg(self.mode, self.n, self.world, self.rank, self.batch, self.num_samples,
-                          self.steps_per_epoch, self.half_bits, self.seed & 0xFFFFFFFFFFFFFFFF)
+                          self.steps_per_epoch, self.bits, self.seed & 0xFFFFFFFFFFFFFFFF)
 
 
 def torch_distributed_indices(n: int, world: int, rank: int, epoch: int, seed: int = 0,

@@ -1,0 +1,59 @@
+"""Phase breakdown of the fused train step from in-kernel s_memtime stamps.
+
+Runs the diagnostic PROF instantiation (toy shape, Adam) for 8 iterations and
+prints the cycles spent between stamps, per iteration, for wave 0 of model 0.
+Stamp instrumentation costs cycles itself: read SHARES, not absolute length.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_pytorch_amd import _native as nat  # noqa: E402
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry  # noqa: E402
+from distributed_training_pytorch_amd.data.toy_data import ToyData  # noqa: E402
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer  # noqa: E402
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC  # noqa: E402
+
+NAMES = ["step_start", "x_loaded", "fwd+loss", "bwd_done(w0)", "tiles_reduced", "grads_summed", "adam_done",
+         "step_end"]
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    X, Y = ToyData(seed=0).device_tensors(dev)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=256), cfg=EngineConfig())
+    tr.train(50)  # warm
+    tr.synchronize()
+    lib = nat.load()
+    prof = torch.zeros(2 * 8 * 16, dtype=torch.int64, device=dev)
+    res = {}
+    for rep in range(3):
+        a = tr._train_args(8, nat.MODE_ADAM, None)
+        a.status = nat.ptr(prof)
+        nat.check(lib.dtp_mlp_train_profile(ctypes.byref(a), nat.stream_ptr()), "profile")
+        torch.cuda.synchronize()
+        st = prof.view(2, 8, 16).cpu()
+        rows = []
+        for it in range(1, 8):
+            s = st[0, it]
+            d = {NAMES[k]: int(s[k] - s[k - 1]) for k in range(1, 8)}
+            d["total_step"] = int(st[0, it, 7] - st[0, it, 0]) if it else 0
+            d["wave_bwd_end_rel"] = [int(st[0, it, 8 + w] - st[0, it, 0]) for w in range(4)]
+            rows.append(d)
+        res[rep] = rows[-1]
+    print(json.dumps(res, indent=1))
+    # also the wall time per step of the plain persistent kernel
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    tr.train(2000)
+    ev1.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"persistent_us_per_step": ev0.elapsed_time(ev1) * 1e3 / 2000}))
+
+
+if __name__ == "__main__":
+    main()
