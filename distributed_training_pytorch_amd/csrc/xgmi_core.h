@@ -79,8 +79,10 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
   // consume every rank's slot from our local buffer, summing in rank order
   const unsigned long long* mine = reinterpret_cast<const unsigned long long*>(a.peers[R]);
   const unsigned long long deadline =
-      __builtin_amdgcn_s_memrealtime() + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 10000000) * 100ull;
-  bool dead = false;
+      __builtin_amdgcn_s_memrealtime() + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
+  // sticky failure: once any exchange of this rank timed out, later ones do not
+  // wait again (a persistent launch must not multiply the timeout by its steps)
+  bool dead = a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
   float acc[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) acc[k] = 0.f;

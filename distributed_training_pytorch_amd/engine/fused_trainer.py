@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native as nat
+from ..parallel import comm_util
 from ..data.sampler import EpochIndexStream, SamplerGeometry
 from ..ops.mlp import MlpSpec, mlp_forward_ref
 from ..ops.optim import OptimConfig, adam_update_ref, flat_optimizer_step, sgd_update_ref
@@ -42,7 +43,8 @@ class EngineConfig:
     loss: str = "mse"            # mse | ce
     log_cap: int = 1 << 16
     cache_data: bool = True
-    xgmi_timeout_us: int = 20_000_000
+    xgmi_timeout_us: int = 2_000_000  # per exchange; sticky once hit (never multiplies over steps)
+    xgmi_selftest: bool = True        # validate the xGMI exchange against a host all-reduce, else fall back
     rccl_graph: bool = True      # capture grad->all_reduce->optimizer into a hipGraph
 
 
@@ -85,29 +87,94 @@ class FusedTrainer:
         self.comm = self._resolve_comm()
         # DDP construction semantics: every rank starts from rank 0's weights
         if self.world > 1:
-            dist.broadcast(self.params, src=0, group=group)
+            comm_util.broadcast_(self.params, 0, group)
         self.native = self.device.type == "cuda" and nat.native_enabled()
         if self.native:
             nat.require(self.device)
             if not spec.native_supported():
                 raise NotImplementedError(f"no fused kernel for {spec}")
         if self.comm == "xgmi":
-            from ..parallel.xgmi import XgmiExchange
-
-            self._xgmi = XgmiExchange(n_models, P, dev, group)
+            self._setup_xgmi()
 
     # ------------------------------------------------------------------ setup
     def _resolve_comm(self) -> str:
         c = self.cfg.comm
-        if self.world == 1:
-            return "none"
         if self.device.type != "cuda":
-            return "gloo"
+            return "gloo" if self.world > 1 else "none"
+        if c == "none" or (self.world == 1 and c == "auto"):
+            if self.world > 1:
+                raise ValueError("comm='none' with world > 1")
+            return "none"
         if c == "auto":
-            return "rccl"
-        if c not in ("rccl", "xgmi"):
+            return "xgmi" if self.world <= 8 else "rccl"
+        if c not in ("rccl", "xgmi", "host"):
             raise ValueError(f"comm {c!r} not valid for a GPU run with world={self.world}")
         return c
+
+    def _setup_xgmi(self):
+        """Map the peers' exchange buffers; self-test; fall back to RCCL on any failure."""
+        from ..parallel.xgmi import XgmiExchange
+
+        ok, why = True, ""
+        try:
+            self._xgmi = XgmiExchange(self.n_models, self.spec.P, self.device, self.group)
+        except Exception as e:  # IPC / peer access unavailable
+            ok, why = False, f"setup: {e}"
+        if ok and self.cfg.xgmi_selftest:
+            try:
+                ok, why = self._xgmi_selftest()
+            except Exception as e:
+                ok, why = False, f"selftest: {e}"
+        if self.world > 1:
+            flag = torch.tensor([0.0 if ok else 1.0], device="cpu")
+            comm_util.all_reduce_(flag, self.group)  # every rank must agree on the path
+            ok = flag.item() == 0.0
+        if not ok:
+            if self.rank == 0:
+                print(f"[dtp] xGMI exchange unavailable ({why or 'a peer failed'}); using RCCL", flush=True)
+            if self._xgmi is not None:
+                if dist.is_initialized():
+                    comm_util.barrier(self.group)
+                self._xgmi.close()
+                self._xgmi = None
+            self.comm = "rccl"
+
+    def _xgmi_selftest(self) -> tuple[bool, str]:
+        """Two exchanges of known values through the real kernel path: one fused
+        step in MODE_XGMI on a scratch copy must reproduce the host all-reduce."""
+        lib = nat.load()
+        saved = [t.clone() for t in (self.params, self.m, self.v, self.step_ctr, self.loss_log)]
+        saved_t = self.t
+        # reference: local grads via MODE_GRAD, host all-reduce, flat optimizer
+        a = self._train_args(1, nat.MODE_GRAD, None)
+        nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
+                  "selftest grad")
+        buf = self.comm_buf.clone()
+        comm_util.all_reduce_(buf, self.group)
+        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.optim,
+                            grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world,
+                            slope=self.spec.slope)
+        ref_p = self.params.clone()
+        ref_l = self.loss_log[0].clone()
+        for t, s0 in zip((self.params, self.m, self.v, self.step_ctr, self.loss_log), saved):
+            t.copy_(s0)
+        # the same step through the in-kernel xGMI exchange (twice: both parities)
+        for _ in range(2):
+            for t, s0 in zip((self.params, self.m, self.v, self.step_ctr, self.loss_log), saved):
+                t.copy_(s0)
+            self._launch(1)
+            torch.cuda.synchronize(self.device)
+            st = self._xgmi.status[:2].tolist()
+            if st[0]:
+                return False, f"timeout at epoch {st[1]}"
+            err = (self.params - ref_p).abs().max().item()
+            lerr = (self.loss_log[0] - ref_l).abs().max().item()
+            if not (err <= 1e-5 and lerr <= 1e-5):
+                return False, f"mismatch vs host all-reduce (param err {err:.3e}, loss err {lerr:.3e})"
+        for t, s0 in zip((self.params, self.m, self.v, self.step_ctr, self.loss_log), saved):
+            t.copy_(s0)
+        self.t = saved_t
+        return True, ""
 
     def _hyper(self, grad_scale: float) -> nat.Hyper:
         return self.optim.hyper(self.spec.slope, grad_scale)
@@ -145,7 +212,7 @@ class FusedTrainer:
             for _ in range(n_steps):
                 self._reference_step()
             return
-        if self.comm == "rccl":
+        if self.comm in ("rccl", "host"):
             for _ in range(n_steps):
                 self._rccl_step()
             return
@@ -210,7 +277,7 @@ class FusedTrainer:
 
     def _rccl_step(self):
         lib = nat.load()
-        if self.cfg.rccl_graph:
+        if self.cfg.rccl_graph and self.comm == "rccl":
             g = self._graphs.get("rccl")
             if g is None:
                 g = self._capture_rccl()
@@ -225,24 +292,25 @@ class FusedTrainer:
         a = self._train_args(1, nat.MODE_GRAD, idx)
         nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
                   "dtp_mlp_train(grad)")
-        dist.all_reduce(self.comm_buf, group=self.group)
+        comm_util.all_reduce_(self.comm_buf, self.group)
         flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, self.comm_buf, self.optim,
                             grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world,
                             slope=self.spec.slope)
 
     def _capture_rccl(self):
         lib = nat.load()
-        # warm the communicator outside capture, then capture one whole step
         try:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self._rccl_body(lib)  # eager warm-up step (counts as a real step)
-            torch.cuda.current_stream().wait_stream(s)
-            self.t += 1
+                # communicator warm-up on a scratch buffer (no training state touched)
+                scratch = torch.zeros_like(self.comm_buf)
+                comm_util.all_reduce_(scratch, self.group)
+            s.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 self._rccl_body(lib)
+            torch.cuda.current_stream().wait_stream(s)
             self._graphs["rccl"] = g
             return g
         except Exception as e:  # capture of collectives unsupported -> eager
@@ -270,7 +338,7 @@ class FusedTrainer:
             losses.append(loss.detach().reshape(1))
         buf = torch.cat([torch.stack(grads).reshape(-1), torch.cat(losses)])
         if self.world > 1:
-            dist.all_reduce(buf, group=self.group)
+            comm_util.all_reduce_(buf, self.group)
         flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.optim,
                             grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world)
         self.t += 1
@@ -313,6 +381,6 @@ class FusedTrainer:
         self._graphs.clear()
         if self._xgmi is not None:
             if dist.is_initialized():
-                dist.barrier(group=self.group)
+                comm_util.barrier(self.group)
             self._xgmi.close()
             self._xgmi = None

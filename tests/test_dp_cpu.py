@@ -1,0 +1,87 @@
+"""Data-parallel semantics on CPU with gloo (world_size 2): init broadcast,
+gradient averaging == single-process average of the per-rank batch gradients,
+replica consistency, global mean loss."""
+import torch
+
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry, torch_distributed_indices
+from distributed_training_pytorch_amd.data.toy_data import ToyData
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, mlp_forward_ref
+from distributed_training_pytorch_amd.ops.optim import OptimConfig, adam_update_ref
+
+from .dist_utils import run_ranks
+
+STEPS = 5
+
+
+def _init(seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(TOY_SPEC.P, generator=g) * 0.3 for _ in range(2)]
+
+
+def _rank_fn(rank, world, steps):
+    ds = ToyData(n=512, seed=1)
+    geom = SamplerGeometry(n=512, world=world, rank=rank, batch=128, seed=3)
+    tr = FusedTrainer(TOY_SPEC, 2, ds.X, ds.Y, geom, OptimConfig(lr=1e-2), EngineConfig(),
+                      init_params=_init(100 + rank))  # different local init: broadcast must win
+    tr.train(steps)
+    return tr.params.clone(), tr.losses(0, steps)
+
+
+def _reference(world, steps):
+    ds = ToyData(n=512, seed=1)
+    geoms = [SamplerGeometry(n=512, world=world, rank=r, batch=128, seed=3) for r in range(world)]
+    params = torch.stack(_init(100))
+    m = torch.zeros_like(params)
+    v = torch.zeros_like(params)
+    cfg = OptimConfig(lr=1e-2)
+    losses = []
+    for t in range(steps):
+        row = []
+        for i in range(2):
+            gs, ls = [], []
+            for g in geoms:
+                idx = torch.tensor(g.indices(t))
+                p = params[i].clone().requires_grad_(True)
+                loss = torch.nn.functional.mse_loss(mlp_forward_ref(p, TOY_SPEC, ds.X[idx]), ds.Y[idx])
+                (gr,) = torch.autograd.grad(loss, p)
+                gs.append(gr)
+                ls.append(loss.item())
+            with torch.no_grad():
+                adam_update_ref(params[i], m[i], v[i], torch.stack(gs).mean(0), t + 1, cfg)
+            row.append(sum(ls) / world)
+        losses.append(row)
+    return params, torch.tensor(losses)
+
+
+def test_fused_trainer_gloo_dp_matches_single_process_average():
+    res = run_ranks(_rank_fn, 2, (STEPS,))
+    ref_p, ref_l = _reference(2, STEPS)
+    p0, l0 = res[0]
+    p1, l1 = res[1]
+    assert torch.equal(p0, p1), "replicas diverged"
+    torch.testing.assert_close(p0, ref_p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(l0, ref_l, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(l1, ref_l, rtol=1e-5, atol=1e-6)
+
+
+def test_device_sampler_partitions_each_epoch():
+    for n, W in [(512, 2), (512, 8), (1000, 3)]:
+        seen = []
+        for r in range(W):
+            g = SamplerGeometry(n=n, world=W, rank=r, batch=64, seed=9)
+            for t in range(g.steps_per_epoch):
+                seen += g.indices(t)
+        total = -(-n // W) * W
+        assert len(seen) == total
+        assert set(seen) == set(range(n))
+
+
+def test_torch_order_matches_distributed_sampler():
+    from torch.utils.data import DistributedSampler
+
+    ds = list(range(100))
+    for W, r, e in [(1, 0, 0), (3, 1, 2), (8, 7, 5)]:
+        s = DistributedSampler(ds, num_replicas=W, rank=r, shuffle=True, seed=4)
+        s.set_epoch(e)
+        assert list(iter(s)) == torch_distributed_indices(100, W, r, e, seed=4)
