@@ -1,0 +1,256 @@
+"""The demo training loop shared by demo.py and demo_assume_started_with_mpiexec.py.
+
+Reference: ``demo.py:19-137`` / ``demo_assume_started_with_mpiexec.py:29-127``:
+two ToyModels (X, Y) trained on ToyData with DDP + Adam + MSE for 1000
+iterations, the global mean loss of each model reduced every iteration and
+logged by rank 0 (``loss/lossX``, ``loss/lossY``), tqdm on rank 0, rank-prefixed
+status prints.
+
+Engines (``--engine``):
+* ``fused``  -- FusedTrainer: the whole iteration in one kernel (or one persistent
+                kernel for many iterations); gradient all-reduce in-kernel over
+                xGMI or through RCCL; losses read lazily from a device ring.
+* ``module`` -- nn.Module path: ModelBank (both models in one flat buffer) with fused
+                per-op kernels, FlatDDP (bucketed RCCL all-reduce overlapped with
+                backward), FlatOptimizer (one Adam launch for both models).
+* ``stock``  -- plain PyTorch eager DDP, the reference loop verbatim (baseline).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..data.sampler import EpochIndexStream, SamplerGeometry
+from ..data.toy_data import ToyData
+from ..ops.optim import OptimConfig
+from ..parallel import comm_util
+from ..runtime import bootstrap, checkpoint
+from ..runtime.errors import FaultInjector, check_replicas
+from ..utils.logging import MetricLogger, rank_print
+
+
+def setup(config, launcher: str | None = None, gpus_per_proc: int = 1):
+    """Discover ranks, bind the device, init the process group, print the reference's status lines."""
+    bootstrap.configure_collective_env()
+    if launcher == "mpi":
+        env = bootstrap.detect(torchrun=False)
+        if env.launcher == "single" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise RuntimeError("expected an MPI launch (OMPI_/PMI_ rank variables not found)")
+    else:
+        env = bootstrap.detect(torchrun=True if config.torchrun else None, use_node_rank=config.use_node_rank)
+    device = bootstrap.bind_device(env, config.device, gpus_per_proc)
+    backend = config.backend
+    if device.type == "cpu" and backend == "nccl":
+        backend = "gloo"
+    bootstrap.init_process_group(env, backend, device, datetime.timedelta(minutes=config.timeout_min))
+    rank, world = dist.get_rank(), dist.get_world_size()
+    # the reference draws --seed independently in every process (argument_parser.py:17)
+    # and never applies it; here rank 0's seed is broadcast so the data and model init
+    # agree across ranks, and each worker gets seed + rank for its own randomness
+    seed_t = torch.tensor([config.seed], dtype=torch.int64)
+    comm_util.broadcast_(seed_t, 0)
+    config.seed = int(seed_t.item())
+    if rank == 0:
+        rank_print(rank, f"World_size: {world}")
+    rank_print(rank, f"Hello from {socket.gethostname()}")
+    if env.local_rank == 0:
+        n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        rank_print(rank, f"Available devices on machine: {n}")
+    base_seed = config.seed
+    worker_seed = base_seed + rank
+    rank_print(rank, f"Base seed: {base_seed} and  worker seed: {worker_seed}")
+    torch.manual_seed(worker_seed)
+    rank_print(rank, f"Using torchrun: {config.torchrun}")
+    rank_print(rank, f"Using backend: {dist.get_backend()}")
+    rank_print(rank, f"Launcher: {env.launcher}; device: {device}")
+    return env, device, rank, world
+
+
+def _dataset(config, rank):
+    return ToyData(n=config.n_samples, seed=config.seed, rank=rank, per_rank=config.per_rank_data,
+                   classes=4 if config.loss == "ce" else 0)
+
+
+def _geom(config, rank, world):
+    return SamplerGeometry(n=config.n_samples, world=world, rank=rank, batch=config.batch_size,
+                           shuffle=True, distributed=config.dataloader == "distributed", seed=0)
+
+
+def _optim(config) -> OptimConfig:
+    return OptimConfig(config.optimizer, config.lr, momentum=config.momentum, weight_decay=config.weight_decay)
+
+
+def _progress(rank, total, config):
+    if rank != 0 or config.no_progress:
+        return None
+    try:
+        from tqdm import tqdm
+
+        return tqdm(total=total, desc="Iteration")
+    except ImportError:  # pragma: no cover
+        return None
+
+
+def train(config, env, device, rank, world, group: str = "base-demo") -> dict:
+    logger = MetricLogger(project=config.project, group=group, log_dir=config.log_dir, rank=rank,
+                          config={k: v for k, v in vars(config).items() if isinstance(v, (int, float, str, bool))})
+    faults = FaultInjector(config.fail_at_iter, config.fail_rank, rank)
+    t_start = time.perf_counter()
+    if config.engine == "fused":
+        summary = _train_fused(config, device, rank, world, logger, faults)
+    elif config.engine == "module":
+        summary = _train_module(config, device, rank, world, logger, faults)
+    else:
+        summary = _train_stock(config, device, rank, world, logger, faults)
+    wall = time.perf_counter() - t_start
+    logger.finish()
+    summary["wall_s"] = wall
+    rank_print(rank, "Finished")
+    return summary
+
+
+# ----------------------------------------------------------------------------- fused engine
+def _train_fused(config, device, rank, world, logger, faults) -> dict:
+    from ..engine.fused_trainer import EngineConfig, FusedTrainer
+    from ..models.toy import ToyModel
+    from ..ops.mlp import MlpSpec
+
+    ds = _dataset(config, rank)
+    X, Y = ds.device_tensors(device)
+    geom = _geom(config, rank, world)
+    torch.manual_seed(config.seed)
+    out_f = 4 if config.loss == "ce" else 1
+    spec = MlpSpec(2, config.hidden, config.depth + 2, out_f)
+    init = [ToyModel(hidden=config.hidden, depth=config.depth, out_features=out_f).flat_params.detach().clone()
+            for _ in range(2)]
+    ecfg = EngineConfig(comm=config.comm, launch=config.launch, steps_per_launch=config.steps_per_launch,
+                        sampler=config.sampler, loss=config.loss)
+    tr = FusedTrainer(spec, 2, X, Y, geom, _optim(config), ecfg, init_params=init)
+    start = 0
+    if config.resume and config.checkpoint_dir:
+        st = checkpoint.load(config.checkpoint_dir)
+        if st is not None:
+            tr.load_state_dict(st)
+            start = tr.t
+            rank_print(rank, f"resumed from {config.checkpoint_dir} at iteration {start}")
+    rank_print(rank, f"engine: fused ({tr.comm} comm, {config.launch} launch)")
+    pbar = _progress(rank, config.iters, config)
+    if pbar is not None and start:
+        pbar.update(start)
+    it = start
+    chunk = max(1, min(config.log_every, config.steps_per_launch))
+    t0 = time.perf_counter()
+    while it < config.iters:
+        n = min(chunk, config.iters - it)
+        if faults.armed() and it <= config.fail_at_iter < it + n:
+            n = config.fail_at_iter - it
+        if n > 0:
+            tr.train(n)
+            ls = tr.losses(it, it + n)  # one host sync per chunk
+            for k in range(n):
+                logger.log({"loss/lossX": ls[k, 0].item()}, step=it + k, commit=False)
+                logger.log({"loss/lossY": ls[k, 1].item()}, step=it + k)
+            it += n
+            if pbar is not None:
+                pbar.update(n)
+        faults.check(it)
+        if config.checkpoint_dir and config.checkpoint_every and it % config.checkpoint_every == 0:
+            tr.synchronize()
+            checkpoint.save({**tr.state_dict(), "config": vars(config)}, config.checkpoint_dir, it)
+    tr.synchronize()
+    dt = time.perf_counter() - t0
+    if pbar is not None:
+        pbar.close()
+    if config.check_replicas:
+        check_replicas(tr.params)
+    if config.checkpoint_dir:
+        checkpoint.save({**tr.state_dict(), "config": vars(config)}, config.checkpoint_dir, it)
+    final = tr.losses(it - 1, it)[0].tolist() if it > 0 else [float("nan")] * 2
+    samples = geom.batch * (it - start) * world
+    tr.close()
+    return {"final_loss": final, "iters": it, "samples_per_s": samples / max(dt, 1e-9), "engine": "fused"}
+
+
+# ----------------------------------------------------------------------------- module engine
+def _train_module(config, device, rank, world, logger, faults) -> dict:
+    from ..models.bank import ModelBank
+    from ..ops.optim import FlatOptimizer
+    from ..parallel.ddp import FlatDDP
+
+    ds = _dataset(config, rank)
+    X, Y = ds.device_tensors(device)
+    geom = _geom(config, rank, world)
+    idx_stream = EpochIndexStream(geom) if config.sampler == "torch" else None
+    torch.manual_seed(config.seed)
+    out_f = 4 if config.loss == "ce" else 1
+    bank = ModelBank(2, hidden=config.hidden, depth=config.depth, out_features=out_f).to(device)
+    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad)
+    opt = FlatOptimizer(bank.flat, bank.flat_grad, _optim(config))
+    lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else torch.nn.MSELoss()
+    pbar = _progress(rank, config.iters, config)
+    t0 = time.perf_counter()
+    lbuf = torch.zeros(2, device=device)
+    for it in range(config.iters):
+        faults.check(it)
+        idx = idx_stream.indices(it) if idx_stream is not None else geom.indices(it)
+        idx_t = torch.tensor(idx, device=device)
+        x, y = X[idx_t], Y[idx_t]
+        if config.loss == "ce":
+            y = y.view(-1).long()
+        bank.zero_grad()
+        ox, oy = ddp(x)
+        lx, ly = lossf(ox, y), lossf(oy, y)
+        (lx + ly).backward()  # independent models: one backward, one bucketed all-reduce
+        opt.step()
+        lbuf[0], lbuf[1] = lx.detach(), ly.detach()
+        comm_util.all_reduce_(lbuf)
+        lbuf.mul_(1.0 / world)
+        if rank == 0:
+            logger.log({"loss/lossX": lbuf[0].item()}, step=it, commit=False)
+            logger.log({"loss/lossY": lbuf[1].item()}, step=it)
+        if pbar is not None:
+            pbar.update(1)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    if pbar is not None:
+        pbar.close()
+    if config.check_replicas:
+        check_replicas(bank.flat)
+    return {"final_loss": lbuf.tolist(), "iters": config.iters,
+            "samples_per_s": geom.batch * config.iters * world / max(dt, 1e-9), "engine": "module"}
+
+
+# ----------------------------------------------------------------------------- stock engine
+def _train_stock(config, device, rank, world, logger, faults) -> dict:
+    from ..baselines.stock import StockLoop
+
+    ds = _dataset(config, rank)
+    loop = StockLoop(ds, device, batch=config.batch_size, seed=config.seed)
+    pbar = _progress(rank, config.iters, config)
+    t0 = time.perf_counter()
+    for it in range(config.iters):
+        faults.check(it)
+        loop.step()
+        if rank == 0:
+            logger.log({"loss/lossX": loop.last[0]}, step=it, commit=False)
+            logger.log({"loss/lossY": loop.last[1]}, step=it)
+        if pbar is not None:
+            pbar.update(1)
+    dt = time.perf_counter() - t0
+    if pbar is not None:
+        pbar.close()
+    loop.close()
+    return {"final_loss": list(loop.last), "iters": config.iters,
+            "samples_per_s": loop.samples * world / max(dt, 1e-9), "engine": "stock"}
+
+
+def teardown():
+    if dist.is_initialized():
+        comm_util.barrier()
+        dist.destroy_process_group()

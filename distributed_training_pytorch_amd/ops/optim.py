@@ -94,3 +94,41 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
         if loss_log is not None:
             loss_log[t % loss_log.shape[0], i] = grad[n_models * P + i] * loss_scale
         step[i] = t + 1
+
+
+class FlatOptimizer:
+    """Adam/SGD over flat [n_models, P] (or [P]) params + grads in one kernel launch
+    (replaces the reference's two torch.optim.Adam, each ~7 kernels x 10 tensors)."""
+
+    def __init__(self, flat_params: torch.Tensor, flat_grad: torch.Tensor, cfg: OptimConfig | None = None,
+                 slope: float = 0.01):
+        self.params = flat_params if flat_params.dim() == 2 else flat_params.view(1, -1)
+        self.grad = flat_grad if flat_grad.dim() == 2 else flat_grad.view(1, -1)
+        self.cfg = cfg or OptimConfig()
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.step_ctr = torch.zeros(self.params.shape[0], dtype=torch.int32, device=self.params.device)
+        n, P = self.params.shape
+        self._buf = torch.zeros(n * P + n, dtype=self.params.dtype, device=self.params.device)
+        self.slope = slope
+
+    @torch.no_grad()
+    def step(self) -> None:
+        n, P = self.params.shape
+        if self.grad.is_contiguous() and self.grad.data_ptr() == self._buf.data_ptr():
+            buf = self._buf
+        else:
+            self._buf[: n * P].copy_(self.grad.reshape(-1))
+            buf = self._buf
+        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.cfg, slope=self.slope)
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        self.grad.zero_()
+
+    def state_dict(self) -> dict:
+        return {"m": self.m.cpu(), "v": self.v.cpu(), "step": self.step_ctr.cpu()}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.step_ctr.copy_(sd["step"])

@@ -1,0 +1,161 @@
+"""Launch modes on CPU (gloo): bootstrap env parsing, torchrun, srun-style SLURM
+env, mpiexec-style MPI env (rendezvous file, no mpi4py), fault injection with
+torchrun --max-restarts + checkpoint resume."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from distributed_training_pytorch_amd.runtime import bootstrap
+
+ROOT = Path(__file__).resolve().parents[1]
+PY = sys.executable
+
+
+def _free_port():
+    return bootstrap.free_port()
+
+
+def test_detect_torchrun():
+    e = bootstrap.detect(env={"RANK": "3", "WORLD_SIZE": "8", "LOCAL_RANK": "1", "LOCAL_WORLD_SIZE": "4",
+                              "MASTER_ADDR": "h0", "MASTER_PORT": "1234", "TORCHELASTIC_RUN_ID": "x"})
+    assert (e.launcher, e.rank, e.world_size, e.local_rank, e.local_world_size) == ("torchrun", 3, 8, 1, 4)
+    with pytest.raises(RuntimeError):
+        bootstrap.detect(torchrun=True, env={"LOCAL_RANK": "0"})
+
+
+def test_detect_slurm_procid_and_node_rank():
+    base = {"SLURM_PROCID": "5", "SLURM_LOCALID": "1", "TASKS_PER_NODE": "4", "WORLD_SIZE": "8",
+            "MASTER_ADDR": "n1", "MASTER_PORT": "2345"}
+    e = bootstrap.detect(env=base)
+    assert (e.launcher, e.rank, e.local_rank, e.local_world_size) == ("slurm", 5, 1, 4)
+    assert e.init_method == "tcp://n1:2345"
+    e2 = bootstrap.detect(use_node_rank=True, env={**base, "NODE_RANK": "1"})
+    assert e2.rank == 1 * 4 + 1
+    e3 = bootstrap.detect(env={"SLURM_PROCID": "2", "SLURM_LOCALID": "0", "SLURM_TASKS_PER_NODE": "2(x3)",
+                               "SLURM_NTASKS": "6", "MASTER_ADDR": "a", "MASTER_PORT": "1"})
+    assert (e3.rank, e3.world_size, e3.local_world_size) == (2, 6, 2)
+    with pytest.raises(ValueError):
+        bootstrap.detect(env={"SLURM_PROCID": "0", "SLURM_LOCALID": "0", "TASKS_PER_NODE": "1", "WORLD_SIZE": "1"})
+
+
+def test_detect_mpi_flavours(tmp_path):
+    e = bootstrap.detect(env={"OMPI_COMM_WORLD_RANK": "3", "OMPI_COMM_WORLD_SIZE": "4",
+                              "OMPI_COMM_WORLD_LOCAL_RANK": "1", "OMPI_COMM_WORLD_LOCAL_SIZE": "2",
+                              "MASTER_ADDR": "m", "MASTER_PORT": "9"})
+    assert (e.launcher, e.rank, e.world_size, e.local_rank, e.local_world_size) == ("mpi", 3, 4, 1, 2)
+    # MPICH/PMI without a local rank: TASKS_PER_NODE fallback (reference :40-41)
+    e = bootstrap.detect(env={"PMI_RANK": "5", "PMI_SIZE": "6", "TASKS_PER_NODE": "2", "MASTER_ADDR": "m",
+                              "MASTER_PORT": "9"})
+    assert (e.rank, e.local_rank) == (5, 1)
+    # rendezvous file when neither mpi4py nor MASTER_* is available
+    f = tmp_path / "rdzv"
+    e = bootstrap.detect(env={"PMI_RANK": "0", "PMI_SIZE": "2", "DTP_RENDEZVOUS_FILE": str(f)})
+    assert f.exists() and e.master_port > 0
+
+
+def test_detect_single():
+    assert bootstrap.detect(env={}).launcher == "single"
+
+
+def _run(cmd, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    env.pop("RANK", None)
+    env.update({"PYTHONPATH": str(ROOT), "OMP_NUM_THREADS": "1", "WANDB_MODE": "disabled"})
+    if env_extra:
+        env.update(env_extra)
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+COMMON = ["--backend", "gloo", "--device", "cpu", "--iters", "20", "--log_every", "5", "--no_progress",
+          "--seed", "11", "--check_replicas"]
+
+
+def _summary(out: str) -> dict:
+    line = [l for l in out.splitlines() if "summary:" in l][-1]
+    return eval(line.split("summary:", 1)[1])  # our own printed dict
+
+
+def test_torchrun_demo_two_ranks():
+    r = _run([PY, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--master-addr",
+              "127.0.0.1", "--master-port", str(_free_port()), "demo.py", "--torchrun", *COMMON])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("Finished") == 2
+    assert _summary(r.stdout)["iters"] == 20
+
+
+def _spawn_env_launch(script, envs, extra_args=()):
+    procs = []
+    base = dict(os.environ)
+    base.pop("RANK", None)
+    base.update({"PYTHONPATH": str(ROOT), "OMP_NUM_THREADS": "1", "WANDB_MODE": "disabled"})
+    for e in envs:
+        procs.append(subprocess.Popen([PY, script, *COMMON, *extra_args], cwd=ROOT, env={**base, **e},
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    return outs
+
+
+def test_srun_style_slurm_env():
+    port = str(_free_port())
+    envs = [{"SLURM_PROCID": str(r), "SLURM_LOCALID": str(r), "TASKS_PER_NODE": "2", "WORLD_SIZE": "2",
+             "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port} for r in range(2)]
+    outs = _spawn_env_launch("demo.py", envs)
+    assert "Launcher: slurm" in outs[0][0]
+    assert _summary(outs[0][0])["iters"] == 20
+
+
+def test_srun_style_use_node_rank():
+    port = str(_free_port())
+    # two "nodes" with one task each: rank = NODE_RANK * TASKS_PER_NODE + SLURM_LOCALID
+    envs = [{"SLURM_PROCID": "0", "SLURM_LOCALID": "0", "NODE_RANK": str(n), "TASKS_PER_NODE": "1",
+             "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port} for n in range(2)]
+    outs = _spawn_env_launch("demo.py", envs, ["--use_node_rank"])
+    assert any("World_size: 2" in o for o, _ in outs)
+
+
+def test_mpiexec_style_env_with_rendezvous_file(tmp_path):
+    f = tmp_path / "rdzv.txt"
+    envs = [{"OMPI_COMM_WORLD_RANK": str(r), "OMPI_COMM_WORLD_SIZE": "2", "OMPI_COMM_WORLD_LOCAL_RANK": str(r),
+             "OMPI_COMM_WORLD_LOCAL_SIZE": "2", "DTP_RENDEZVOUS_FILE": str(f)} for r in range(2)]
+    outs = _spawn_env_launch("demo_assume_started_with_mpiexec.py", envs)
+    assert "Launcher: mpi" in outs[0][0]
+    s = _summary(outs[0][0])
+    assert s["iters"] == 20 and all(v == v for v in s["final_loss"])
+
+
+def test_fault_injection_restart_resume(tmp_path):
+    ck = tmp_path / "ck"
+    r = _run([PY, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--master-addr",
+              "127.0.0.1", "--master-port", str(_free_port()), "--max-restarts", "1", "demo.py", "--torchrun",
+              *COMMON, "--iters", "40", "--checkpoint_dir", str(ck), "--checkpoint_every", "10", "--resume",
+              "--fail_at_iter", "25", "--log_dir", str(tmp_path / "logs")],
+             env_extra={"TORCHELASTIC_ERROR_FILE": str(tmp_path / "err.json")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "resumed from" in r.stdout and "at iteration 20" in r.stdout
+    assert _summary(r.stdout)["iters"] == 40
+    assert (ck / "last.pt").exists()
+    rows = [json.loads(l) for l in open(tmp_path / "logs" / "metrics.jsonl")]
+    assert any(row.get("step") == 39 for row in rows)
+
+
+def test_error_file_written(tmp_path):
+    from distributed_training_pytorch_amd.runtime.errors import record
+
+    os.environ["TORCHELASTIC_ERROR_FILE"] = str(tmp_path / "e.json")
+    try:
+        @record
+        def boom():
+            raise ValueError("x")
+
+        with pytest.raises(ValueError):
+            boom()
+        d = json.load(open(tmp_path / "e.json"))
+        assert "ValueError" in d["message"]["message"]
+    finally:
+        del os.environ["TORCHELASTIC_ERROR_FILE"]
