@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Lightning-style demo: two ToyModels, two Adams, DDP strategy.
+
+Reference: demo_pytorch_lightning.py (``pl.Trainer(gpus, num_nodes, max_steps,
+precision=32, accelerator='gpu', strategy='ddp')``, backend from
+PL_TORCH_DISTRIBUTED_BACKEND, launched one task per GPU by srun).  Uses the in-repo
+Trainer (distributed_training_pytorch_amd.trainer), which follows PyTorch-Lightning
+1.5.10 semantics; when pytorch_lightning is importable and ``--use_lightning`` is
+given, the real Lightning Trainer is used instead.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+from torch.utils.data import DataLoader  # noqa: E402
+
+from distributed_training_pytorch_amd.runtime.errors import record  # noqa: E402
+from distributed_training_pytorch_amd.trainer import LightningModule, Trainer  # noqa: E402
+from toy_model_and_data import ToyData, ToyModel  # noqa: E402
+
+
+class LitToyModel(LightningModule):
+    def __init__(self, lr: float = 1e-3):
+        super().__init__()
+        self.model_X = ToyModel()
+        self.model_Y = ToyModel()
+        self.loss = nn.MSELoss()
+        self.lr = lr
+
+    def forward(self, x):
+        return self.model_X(x), self.model_Y(x)
+
+    def training_step(self, batch, batch_idx, optimizer_idx=0):
+        x, y = batch
+        out_x, out_y = self(x)
+        loss_x = self.loss(out_x, y)
+        loss_y = self.loss(out_y, y)
+        self.log("loss/lossX", loss_x)
+        self.log("loss/lossY", loss_y)
+        return loss_x + loss_y
+
+    def configure_optimizers(self):
+        return [torch.optim.Adam(self.model_X.parameters(), lr=self.lr),
+                torch.optim.Adam(self.model_Y.parameters(), lr=self.lr)]
+
+
+def get_args(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--nnodes", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--num_workers", type=int, default=0)
+    p.add_argument("--batch_size", type=int, default=128)
+    p.add_argument("--accelerator", choices=["gpu", "cpu"], default=None)
+    p.add_argument("--root_dir", type=str, default=None)
+    p.add_argument("--no_progress", action="store_true")
+    p.add_argument("--use_lightning", action="store_true", help="use pytorch_lightning if it is installed")
+    return p.parse_args(argv)
+
+
+@record
+def main(argv=None):
+    a = get_args(argv)
+    torch.manual_seed(a.seed)
+    ds = ToyData(seed=a.seed)
+    dl = DataLoader(ds, batch_size=a.batch_size, pin_memory=torch.cuda.is_available(), num_workers=a.num_workers)
+    model = LitToyModel()
+    accel = a.accelerator or ("gpu" if torch.cuda.is_available() else "cpu")
+    TrainerCls = Trainer
+    if a.use_lightning:
+        try:
+            import pytorch_lightning as pl
+
+            TrainerCls = pl.Trainer
+        except ImportError:
+            print("pytorch_lightning not installed; using the in-repo Trainer", flush=True)
+    trainer = TrainerCls(gpus=a.gpus, num_nodes=a.nnodes, max_steps=a.steps, precision=32, accelerator=accel,
+                         log_every_n_steps=min(50, len(dl) / a.batch_size), strategy="ddp",
+                         default_root_dir=a.root_dir, enable_progress_bar=not a.no_progress, seed=a.seed)
+    trainer.fit(model, dl)
+    if getattr(trainer, "global_rank", 0) == 0:
+        print(f"[Process 0] summary: {{'global_step': {trainer.global_step}, 'metrics': {trainer.callback_metrics}, "
+              f"'checkpoint': {trainer.checkpoint_path!r}}}", flush=True)
+    if hasattr(trainer, "teardown"):
+        trainer.teardown()
+
+
+if __name__ == "__main__":
+    main()

@@ -93,6 +93,7 @@ class StageArgs(ctypes.Structure):
         ("grad_out", c_void_p),
         ("grad_in", c_void_p),
         ("grad_params", c_void_p),
+        ("out_peer", c_void_p),
         ("batch", c_int),
         ("slope", c_float),
     ]

@@ -62,6 +62,8 @@ struct DtpStageArgs {
   const float* grad_out;  // [B][OUT]  (backward)
   float* grad_in;         // [B][IN]   (backward, nullable)
   float* grad_params;     // [P]       (backward; must be zeroed when the grid has >1 block)
+  float* out_peer;        // [B][OUT]  forward: second copy of the output stored straight into
+                          //           the next stage's GPU (peer-mapped over xGMI), nullable
   int batch;
   float slope;
 };

@@ -23,6 +23,11 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_fwd_kernel(DtpStageArgs a) {
   static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = a.x[(size_t)b * S::IN + decltype(IC)::value]; });
   mlp_forward<S>(sw, h, a.slope);
   static_for<0, S::OUT>([&](auto JC) { a.out[(size_t)b * S::OUT + decltype(JC)::value] = h[S::NL][decltype(JC)::value]; });
+  if (a.out_peer) {  // layer-split hand-off: the epilogue writes the next GPU's input directly
+    static_for<0, S::OUT>([&](auto JC) {
+      a.out_peer[(size_t)b * S::OUT + decltype(JC)::value] = h[S::NL][decltype(JC)::value];
+    });
+  }
   if (a.saved) {
     static_for<1, S::NL>([&](auto LC) {
       constexpr int l = decltype(LC)::value;

@@ -112,8 +112,11 @@ def _check_f32_cuda(name: str, t: torch.Tensor, device: torch.device, numel: int
         raise ValueError(f"{name} must have {numel} elements, got {t.numel()}")
 
 
-def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool = True):
-    """Native forward of one MLP stage. Returns (out [B,OUT], saved [B,(NL-1)*H] or None)."""
+def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool = True,
+                  peer_device: torch.device | None = None):
+    """Native forward of one MLP stage. Returns (out [B,OUT], saved [B,(NL-1)*H] or None)
+    or, with peer_device, (out, saved, out_peer) where out_peer lives on peer_device and is
+    written by the same kernel over xGMI (peer access must be enabled)."""
     lib = nat.require(x.device)
     if x.dim() != 2 or x.shape[1] != spec.in_features:
         raise ValueError(f"input must be [B, {spec.in_features}], got {tuple(x.shape)}")
@@ -124,8 +127,14 @@ def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool
     out = torch.empty(B, spec.out_features, device=dev, dtype=torch.float32)
     saved = torch.empty(B, (spec.n_layers - 1) * spec.hidden, device=dev, dtype=torch.float32) \
         if (save and spec.n_layers > 1) else None
-    a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), None, None, None, B, spec.slope)
+    out_peer = None
+    if peer_device is not None and torch.device(peer_device) != dev:
+        out_peer = torch.empty(B, spec.out_features, device=peer_device, dtype=torch.float32)
+    a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), None, None, None, nat.ptr(out_peer),
+                      B, spec.slope)
     nat.check(lib.dtp_mlp_stage_fwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_fwd")
+    if peer_device is not None:
+        return out, saved, (out_peer if out_peer is not None else out)
     return out, saved
 
 
@@ -135,13 +144,16 @@ def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: b
     dev = x.device
     B = x.shape[0]
     grad_out = grad_out.contiguous()
-    _check_f32_cuda("grad_out", grad_out, dev, B * spec.out_features)
+    if grad_out.device != dev and grad_out.device.type == "cuda":
+        pass  # peer read over xGMI (layer split): the kernel loads it through the peer mapping
+    else:
+        _check_f32_cuda("grad_out", grad_out, dev, B * spec.out_features)
     grad_in = torch.empty(B, spec.in_features, device=dev, dtype=torch.float32) if need_grad_in else None
     nblk = (B + 1023) // 1024
     gp = torch.zeros(spec.P, device=dev, dtype=torch.float32) if nblk > 1 else \
         torch.empty(spec.P, device=dev, dtype=torch.float32)
     a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), nat.ptr(grad_out),
-                      nat.ptr(grad_in), nat.ptr(gp), B, spec.slope)
+                      nat.ptr(grad_in), nat.ptr(gp), None, B, spec.slope)
     nat.check(lib.dtp_mlp_stage_bwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_bwd")
     return grad_in, gp
 

@@ -1,0 +1,235 @@
+"""Trainer: a PyTorch-Lightning-1.5-compatible training driver (the parts the reference
+uses: ``pl.Trainer(gpus, num_nodes, max_steps, precision=32, accelerator='gpu',
+log_every_n_steps, strategy='ddp')`` + ``fit``, ``demo_pytorch_lightning.py:57-62``).
+
+Semantics kept from PL 1.5.10:
+* cluster environment: SLURM (SLURM_PROCID/LOCALID/NODEID/NTASKS + MASTER_ADDR/PORT)
+  or torchrun env, else one process; backend from ``PL_TORCH_DISTRIBUTED_BACKEND``;
+* ``strategy='ddp'``: rank-0 parameter broadcast, gradient averaging on every
+  backward (FlatDDP: flat buffer, bucketed RCCL all-reduce overlapped with the
+  backward, unused-parameter tolerant), DistributedSampler auto-injected into a
+  sampler-less DataLoader;
+* several optimizers: per batch, for each optimizer: toggle (only its params
+  require grad), training_step(batch, batch_idx, optimizer_idx), backward, step,
+  zero_grad; ``global_step`` advances once per BATCH (PL 1.5, not 1.6+);
+* ``log_every_n_steps`` (a float in the reference, 0.03125) is clamped to an int >= 1;
+* default checkpointing: ``{root}/lightning_logs/version_N/checkpoints/
+  epoch={e}-step={s}.ckpt`` at the end of training; CSV metrics alongside.
+MI355X-first: a dataset exposing device tensors (``ToyData``) is gathered on the GPU
+(no collation/pin-memory per batch), the model's layers run as fused HIP kernels.
+"""
+from __future__ import annotations
+
+import csv
+import datetime
+import os
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+from ..data.sampler import SamplerGeometry, torch_distributed_indices
+from ..parallel import comm_util
+from ..parallel.ddp import FlatDDP
+from ..runtime import bootstrap
+from ..utils.logging import rank_print
+
+
+class CSVLogger:
+    def __init__(self, root: str, rank: int):
+        self.rank = rank
+        self.dir = None
+        if rank != 0:
+            return
+        base = Path(root) / "lightning_logs"
+        base.mkdir(parents=True, exist_ok=True)
+        n = 0
+        while (base / f"version_{n}").exists():
+            n += 1
+        self.dir = base / f"version_{n}"
+        self.dir.mkdir(parents=True)
+        self._f = open(self.dir / "metrics.csv", "w", newline="")
+        self._w = None
+
+    def log(self, step: int, metrics: dict):
+        if self.dir is None:
+            return
+        row = {"step": step, **{k: float(v) for k, v in metrics.items()}}
+        if self._w is None:
+            self._w = csv.DictWriter(self._f, fieldnames=list(row.keys()), extrasaction="ignore")
+            self._w.writeheader()
+        self._w.writerow(row)
+        self._f.flush()
+
+    def close(self):
+        if self.dir is not None:
+            self._f.close()
+
+
+class _DeviceBatches:
+    """Device-resident replacement for DataLoader(DistributedSampler(ds), batch_size)."""
+
+    def __init__(self, X, Y, batch, world, rank, shuffle, seed=0):
+        self.X, self.Y = X, Y
+        self.geom = SamplerGeometry(n=X.shape[0], world=world, rank=rank, batch=batch, shuffle=shuffle, seed=seed)
+        self.epoch = 0
+
+    def __len__(self):
+        return self.geom.steps_per_epoch
+
+    def set_epoch(self, e):
+        self.epoch = e
+
+    def __iter__(self):
+        g = self.geom
+        idx = torch_distributed_indices(g.n, g.world, g.rank, self.epoch, g.seed, g.shuffle)
+        idx_t = torch.tensor(idx, device=self.X.device)
+        for b in range(len(self)):
+            sel = idx_t[b * g.batch:(b + 1) * g.batch]
+            yield self.X[sel], self.Y[sel]
+
+
+class Trainer:
+    def __init__(self, gpus: int | None = None, num_nodes: int = 1, max_steps: int = -1, max_epochs: int | None = None,
+                 precision: int = 32, accelerator: str | None = None, strategy: str | None = None,
+                 log_every_n_steps: float = 50, default_root_dir: str | None = None,
+                 enable_checkpointing: bool = True, enable_progress_bar: bool = True, seed: int | None = None,
+                 **unused):
+        if precision not in (32, "32"):
+            raise NotImplementedError("the toy MLP path trains in fp32 (precision=32), like the reference")
+        self.gpus = gpus
+        self.num_nodes = num_nodes
+        self.max_steps = max_steps
+        self.max_epochs = max_epochs if max_epochs is not None else (1000 if max_steps < 0 else None)
+        self.accelerator = accelerator or ("gpu" if torch.cuda.is_available() and gpus else "cpu")
+        self.strategy = strategy
+        self.log_every_n_steps = max(1, int(log_every_n_steps))  # reference passes 0.03125
+        self.root = default_root_dir or os.getcwd()
+        self.enable_checkpointing = enable_checkpointing
+        self.enable_progress_bar = enable_progress_bar
+        self.seed = seed
+        self.global_step = 0
+        self.current_epoch = 0
+        self.callback_metrics: dict = {}
+        self.checkpoint_path: str | None = None
+
+    # ------------------------------------------------------------------ distributed
+    def _setup(self):
+        env = bootstrap.detect()
+        device = torch.device("cpu")
+        if self.accelerator == "gpu" and torch.cuda.is_available():
+            device = bootstrap.bind_device(env, "cuda")
+        if self.strategy in ("ddp", "ddp_spawn", "ddp_find_unused_parameters_false") or env.world_size > 1:
+            backend = os.environ.get("PL_TORCH_DISTRIBUTED_BACKEND", "nccl" if device.type == "cuda" else "gloo")
+            bootstrap.configure_collective_env()
+            bootstrap.init_process_group(env, backend, device, datetime.timedelta(minutes=60))
+        self.env = env
+        self.device = device
+        self.world_size = dist.get_world_size() if dist.is_initialized() else 1
+        self.global_rank = dist.get_rank() if dist.is_initialized() else 0
+        expected = (self.gpus or 1) * self.num_nodes
+        if self.global_rank == 0 and dist.is_initialized() and self.world_size != expected:
+            rank_print(0, f"note: world size {self.world_size} != gpus*num_nodes {expected}")
+
+    def _loader(self, dl):
+        ds = getattr(dl, "dataset", dl)
+        bs = getattr(dl, "batch_size", None) or 1
+        if hasattr(ds, "device_tensors"):
+            X, Y = ds.device_tensors(self.device)
+            return _DeviceBatches(X, Y, bs, self.world_size, self.global_rank, shuffle=self.world_size > 1)
+        if self.world_size > 1 and not isinstance(getattr(dl, "sampler", None),
+                                                   torch.utils.data.distributed.DistributedSampler):
+            from torch.utils.data import DataLoader, DistributedSampler
+
+            s = DistributedSampler(ds, shuffle=True)
+            return DataLoader(ds, batch_size=bs, sampler=s, num_workers=getattr(dl, "num_workers", 0),
+                              pin_memory=self.device.type == "cuda")
+        return dl
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, model, train_dataloaders=None, train_dataloader=None):
+        dl = train_dataloaders if train_dataloaders is not None else train_dataloader
+        self._setup()
+        if self.seed is not None:
+            torch.manual_seed(self.seed)
+        model.trainer = self
+        model.to(self.device)
+        ddp = FlatDDP(model) if self.world_size > 1 else None
+        opts = model.configure_optimizers()
+        if not isinstance(opts, (list, tuple)):
+            opts = [opts]
+        loader = self._loader(dl)
+        logger = CSVLogger(self.root, self.global_rank)
+        pbar = None
+        if self.enable_progress_bar and self.global_rank == 0:
+            try:
+                from tqdm import tqdm
+
+                pbar = tqdm(total=self.max_steps if self.max_steps > 0 else None, desc="Epoch 0")
+            except ImportError:  # pragma: no cover
+                pbar = None
+        model.on_train_start()
+        t0 = time.perf_counter()
+        done = False
+        while not done:
+            if hasattr(loader, "set_epoch"):
+                loader.set_epoch(self.current_epoch)
+            elif hasattr(getattr(loader, "sampler", None), "set_epoch"):
+                loader.sampler.set_epoch(self.current_epoch)
+            for batch_idx, batch in enumerate(loader):
+                batch = [b.to(self.device, non_blocking=True) for b in batch]
+                for oi, opt in enumerate(opts):
+                    if len(opts) > 1:
+                        model.toggle_optimizer(opt, oi, opts)
+                    if ddp is not None:
+                        ddp.zero_grad()
+                    else:
+                        opt.zero_grad(set_to_none=False)
+                    out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
+                        model.training_step(batch, batch_idx)
+                    loss = out["loss"] if isinstance(out, dict) else out
+                    loss.backward()
+                    opt.step()
+                    if len(opts) > 1:
+                        model.untoggle_optimizer(oi)
+                    model._logged[f"train_loss_opt{oi}"] = loss.detach()
+                self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
+                if self.global_step % self.log_every_n_steps == 0:
+                    metrics = {k: v for k, v in model._logged.items()}
+                    vals = torch.stack([v.float().reshape(()) for v in metrics.values()]).to(self.device)
+                    comm_util.all_reduce_(vals)
+                    vals /= self.world_size
+                    self.callback_metrics = dict(zip(metrics.keys(), vals.tolist()))
+                    logger.log(self.global_step, self.callback_metrics)
+                if pbar is not None:
+                    pbar.update(1)
+                if 0 < self.max_steps <= self.global_step:
+                    done = True
+                    break
+            self.current_epoch += 1
+            if self.max_epochs is not None and self.current_epoch >= self.max_epochs:
+                done = True
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.fit_time = time.perf_counter() - t0
+        if pbar is not None:
+            pbar.close()
+        model.on_train_end()
+        if self.enable_checkpointing and logger.dir is not None:
+            ck = logger.dir / "checkpoints"
+            ck.mkdir(exist_ok=True)
+            path = ck / f"epoch={self.current_epoch - 1}-step={self.global_step}.ckpt"
+            tmp = path.with_suffix(".tmp")
+            torch.save({"state_dict": {k: v.detach().cpu() for k, v in model.state_dict().items()},
+                        "global_step": self.global_step, "epoch": self.current_epoch - 1,
+                        "optimizer_states": [o.state_dict() for o in opts]}, tmp)
+            os.replace(tmp, path)
+            self.checkpoint_path = str(path)
+        logger.close()
+        return self
+
+    def teardown(self):
+        if dist.is_initialized():
+            comm_util.barrier()
+            dist.destroy_process_group()

@@ -1,0 +1,79 @@
+"""FlatDDP vs torch DDP, ModelBank packing, and the Lightning-style Trainer (CPU, gloo, 2 ranks)."""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import torch
+
+from distributed_training_pytorch_amd.models.bank import ModelBank
+from distributed_training_pytorch_amd.runtime import bootstrap
+
+from .dist_utils import run_ranks
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _flatddp_vs_ddp(rank, world):
+    import torch.distributed as dist
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(100 + rank)  # different local init: the broadcast must equalise
+    bank = ModelBank(2)
+    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad, first_bucket_mb=0.0005,
+                  bucket_cap_mb=0.001)  # several buckets
+    torch.manual_seed(100 + rank)
+    ref = [torch.nn.Sequential(*[m for m in ModelBank(2)[i].layers]) for i in range(2)]
+    # same start point as the broadcast bank (rank 0's init)
+    for i in range(2):
+        for p, q in zip(ref[i].parameters(), bank[i].parameters()):
+            p.data.copy_(q.data)
+    refd = [DDP(r) for r in ref]
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(64, 2, generator=g)
+    y = torch.randn(64, 1, generator=g)
+    bank.zero_grad()
+    ox, oy = ddp(x)
+    (torch.nn.functional.mse_loss(ox, y) + torch.nn.functional.mse_loss(oy, y)).backward()
+    for r in refd:
+        torch.nn.functional.mse_loss(r(x), y).backward()
+    gref = torch.cat([p.grad.reshape(-1) for r in ref for p in r.parameters()])
+    return bank.flat_grad.reshape(-1).clone(), gref, len(ddp._buckets)
+
+
+def test_flatddp_matches_torch_ddp():
+    res = run_ranks(_flatddp_vs_ddp, 2)
+    for r in range(2):
+        g, gref, nb = res[r]
+        assert nb > 1
+        torch.testing.assert_close(g, gref, rtol=1e-5, atol=1e-7)
+    assert torch.equal(res[0][0], res[1][0])
+
+
+def test_model_bank_views_and_state_dict():
+    torch.manual_seed(0)
+    bank = ModelBank(2)
+    assert bank.flat.shape == (2, 371)
+    w = bank[1].layers[2].weight
+    w.data.fill_(3.0)
+    assert (bank.flat[1, 30:130] == 3.0).all()
+    keys = set(bank[0].state_dict().keys())
+    assert keys == {f"layers.{i}.{k}" for i in (0, 2, 4, 6, 8) for k in ("weight", "bias")}
+
+
+def test_lightning_style_trainer_two_ranks(tmp_path):
+    env = dict(os.environ, PYTHONPATH=str(ROOT), PL_TORCH_DISTRIBUTED_BACKEND="gloo", OMP_NUM_THREADS="1")
+    env.pop("RANK", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(bootstrap.free_port()),
+                        "demo_pytorch_lightning.py", "--steps", "12", "--accelerator", "cpu", "--root_dir",
+                        str(tmp_path), "--no_progress", "--gpus", "2"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "'global_step': 12" in r.stdout
+    ck = list((tmp_path / "lightning_logs" / "version_0" / "checkpoints").glob("*.ckpt"))
+    assert len(ck) == 1 and "step=12" in ck[0].name
+    sd = torch.load(ck[0], weights_only=True)
+    assert "model_X.layers.0.weight" in sd["state_dict"]
