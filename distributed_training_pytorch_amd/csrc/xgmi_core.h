@@ -59,7 +59,7 @@ DTP_DEV float poll_granule(const unsigned long long* p, unsigned epoch, unsigned
 // granules per (model, src rank) slot: P gradient values + 1 loss, 64-byte rounded
 DTP_HD int xgmi_slot_granules(int P) { return (P + 1 + 7) & ~7; }
 
-template <int NPT>
+template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
                                    unsigned epoch, int tid) {
   const int W = a.smp.world, R = a.smp.rank;
@@ -71,7 +71,7 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.peers[r]) + (base + R) * slot;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int p = tid + k * kBlock;
+      const int p = tid + k * NTHREADS;
       if (p < P) store_granule_sys(dst + p, pack_granule(epoch, g[k]));
     }
     if (tid == 0) store_granule_sys(dst + P, pack_granule(epoch, loss));
@@ -91,7 +91,7 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
     const unsigned long long* src = mine + (base + r) * slot;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int p = tid + k * kBlock;
+      const int p = tid + k * NTHREADS;
       if (p < P) acc[k] += poll_granule(src + p, epoch, deadline, dead, a.status);
     }
     if (tid == 0) lacc += poll_granule(src + P, epoch, deadline, dead, a.status);

@@ -29,20 +29,24 @@ def main():
     tr.train(50)  # warm
     tr.synchronize()
     lib = nat.load()
-    prof = torch.zeros(2 * 8 * 16, dtype=torch.int64, device=dev)
+    prof = torch.zeros(2 * 8 * 32, dtype=torch.int64, device=dev)
     res = {}
     for rep in range(3):
         a = tr._train_args(8, nat.MODE_ADAM, None)
         a.status = nat.ptr(prof)
         nat.check(lib.dtp_mlp_train_profile(ctypes.byref(a), nat.stream_ptr()), "profile")
         torch.cuda.synchronize()
-        st = prof.view(2, 8, 16).cpu()
+        st = prof.view(2, 8, 32).cpu()
         rows = []
         for it in range(1, 8):
             s = st[0, it]
             d = {NAMES[k]: int(s[k] - s[k - 1]) for k in range(1, 8)}
             d["total_step"] = int(st[0, it, 7] - st[0, it, 0]) if it else 0
-            d["wave_bwd_end_rel"] = [int(st[0, it, 8 + w] - st[0, it, 0]) for w in range(4)]
+            d["wave_bwd_end_rel"] = [int(st[0, it, 8 + w] - st[0, it, 0]) for w in range(8)]
+            fl = [int(st[0, it, 16 + l]) for l in range(8) if int(st[0, it, 16 + l])]
+            d["fwd_layers"] = [int(b - a) for a, b in zip([int(s[1])] + fl[:-1], fl)]
+            bl = [int(st[0, it, 24 + l]) for l in range(8) if int(st[0, it, 24 + l])][::-1]
+            d["bwd_layers(top->0)"] = [int(b - a) for a, b in zip([int(s[2])] + bl[:-1], bl)]
             rows.append(d)
         res[rep] = rows[-1]
     print(json.dumps(res, indent=1))
