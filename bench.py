@@ -38,10 +38,13 @@ from distributed_training_pytorch_amd.ops.optim import OptimConfig  # noqa: E402
 from distributed_training_pytorch_amd.utils import dist_env  # noqa: E402
 
 METRIC = "samples/sec (whole node) toy MLP DDP at 1/2/4/8 MI355X; scaling efficiency"
-# Stock PyTorch-ROCm eager DDP re-enactment of the reference loop, measured on
-# MI355X with `bench.py --impl stock` (BASELINE.md "measured baseline");
-# None until measured for that N.
-STOCK_BASELINE = {}
+# The reference publishes no numbers, so the baseline is its loop
+# re-enacted on stock PyTorch-ROCm eager (`bench.py --impl stock`), measured on one
+# MI355X: 104,998 samples/s (profiles/r1_bench_stock.json).  For N > 1 the
+# denominator is that number times N -- stock DDP with PERFECT linear scaling,
+# an upper bound on what the stock loop could reach (only 1 GPU is available to
+# measure it on).
+STOCK_SAMPLES_PER_S_1GPU = 104998.36
 
 
 def parse():
@@ -114,7 +117,7 @@ def main():
         final_loss = list(runner.last)
         runner.close()
 
-    base = STOCK_BASELINE.get(world)
+    base = STOCK_SAMPLES_PER_S_1GPU * world
     if rank == 0:
         rec = {
             "metric": METRIC,

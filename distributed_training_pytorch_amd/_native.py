@@ -117,6 +117,35 @@ class OptArgs(ctypes.Structure):
     ]
 
 
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("A", c_void_p),
+        ("B", c_void_p),
+        ("C", c_void_p),
+        ("bias", c_void_p),
+        ("aux", c_void_p),
+        ("lda", c_longlong),
+        ("ldb", c_longlong),
+        ("ldc", c_longlong),
+        ("ldaux", c_longlong),
+        ("M", c_int),
+        ("N", c_int),
+        ("K", c_int),
+        ("dtype", c_int),
+        ("out_dtype", c_int),
+        ("trans_a", c_int),
+        ("trans_b", c_int),
+        ("act", c_int),
+        ("accumulate", c_int),
+        ("splitk", c_int),
+        ("alpha", c_float),
+        ("slope", c_float),
+        ("vec_a", c_int),
+        ("vec_b", c_int),
+    ]
+
+
+DT_F32, DT_BF16 = 0, 1
 MODE_GRAD, MODE_ADAM, MODE_SGD, MODE_XGMI_ADAM, MODE_XGMI_SGD = 0, 1, 2, 3, 4
 LOSS_MSE, LOSS_CE = 0, 1
 SAMPLER_EXPLICIT, SAMPLER_DIST_SHUFFLE, SAMPLER_SEQUENTIAL, SAMPLER_DIST_NOSHUFFLE = 0, 1, 2, 3
@@ -159,6 +188,8 @@ def _declare(lib):
         "dtp_graph_launch": (c_int, [c_void_p, c_void_p]),
         "dtp_graph_destroy": (c_int, [c_void_p]),
         "dtp_struct_sizes": (c_int, [P(c_int)]),
+        "dtp_gemm": (c_int, [P(GemmArgs), c_void_p]),
+        "dtp_colsum": (c_int, [c_void_p, c_longlong, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -189,9 +220,9 @@ def load(build_if_missing: bool = False):
         _declare(lib)
         sizes = (c_int * 8)()
         lib.dtp_struct_sizes(sizes)
-        mine = [ctypes.sizeof(t) for t in (SamplerCfg, Hyper, TrainArgs, StageArgs, OptArgs)]
-        if list(sizes[:5]) != mine:
-            raise NativeUnavailable(f"ABI mismatch between libdtp.so {list(sizes[:5])} and _native.py {mine}: rebuild")
+        mine = [ctypes.sizeof(t) for t in (SamplerCfg, Hyper, TrainArgs, StageArgs, OptArgs, GemmArgs)]
+        if list(sizes[:6]) != mine:
+            raise NativeUnavailable(f"ABI mismatch between libdtp.so {list(sizes[:6])} and _native.py {mine}: rebuild")
         _lib = lib
         return lib
 

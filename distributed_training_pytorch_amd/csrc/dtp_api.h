@@ -90,6 +90,31 @@ struct DtpOptArgs {
 
 int dtp_flat_optimizer(const DtpOptArgs* a, void* stream);
 
+// ---- MFMA GEMM with fused Linear epilogues (gemm.hip) ----
+#define DTP_DT_F32 0
+#define DTP_DT_BF16 1
+struct DtpGemmArgs {
+  const void* A;      // A(m,k) = A[m*lda+k] (trans_a=0) or A[k*lda+m] (trans_a=1)
+  const void* B;      // B(n,k) = B[n*ldb+k] (trans_b=0) or B[k*ldb+n] (trans_b=1)
+  void* C;            // [M][ldc], out_dtype
+  const float* bias;  // [N] or null
+  const void* aux;    // [M][ldaux] (dtype): multiply by LeakyReLU'(aux) (backward through the previous layer)
+  long long lda, ldb, ldc, ldaux;
+  int M, N, K;
+  int dtype;       // DTP_DT_* of A, B, aux
+  int out_dtype;   // DTP_DT_* of C
+  int trans_a, trans_b;
+  int act;         // 1: LeakyReLU(slope) on the result
+  int accumulate;  // 1: C += result
+  int splitk;      // >1: K split over blocks, f32 atomics into C
+  float alpha, slope;
+  int vec_a, vec_b;  // set by dtp_gemm (16-byte loads allowed)
+};
+
+int dtp_gemm(const DtpGemmArgs* a, void* stream);
+// out[n] (+)= sum_m X[m*ld+n]  (bias gradients)
+int dtp_colsum(const void* X, long long ld, int M, int N, int dtype, float* out, int accumulate, void* stream);
+
 // sampler probe (tests): dataset indices of steps [t0, t0+n_steps), row-major [n_steps][batch], -1 padded
 int dtp_sampler_indices(const dtp::SamplerCfg* s, long long t0, int n_steps, int* out, void* stream);
 

@@ -1,0 +1,353 @@
+// LDS-tiled MFMA GEMM for gfx950 (CDNA4) with fused Linear-layer epilogues.
+//
+// C[M,N] (+)= epi( alpha * sum_k A(m,k) * B(n,k) )
+//   A(m,k) = A[m*lda + k] (trans_a = 0)  or  A[k*lda + m] (trans_a = 1)
+//   B(n,k) = B[n*ldb + k] (trans_b = 0)  or  B[k*ldb + n] (trans_b = 1)
+// so the three GEMMs of an MLP layer y = act(x W^T + b) are
+//   forward   y  = x W^T        (0, 0)   epilogue: + bias, LeakyReLU
+//   grad in   dx = dz W         (0, 1)   epilogue: * act'(h_prev)   (h_prev = aux)
+//   grad W    dW = dz^T x       (1, 1)   optional split-K (f32 atomics into C)
+// (the addmm / mm / leaky_relu(_backward) kernels the
+// reference runs through cuBLAS/ATen, `toy_model_and_data.py:12-25`.)
+//
+// MI355X-first design:
+//  * 128x128 block tile, 256 threads = 4 waves (2x2), each wave a 64x64 tile of
+//    4x4 MFMA 16x16 fragments: v_mfma_f32_16x16x32_bf16 for bf16 inputs,
+//    v_mfma_f32_16x16x4_f32 (exact fp32) for f32 inputs.
+//  * the LDS image of both operands is K-contiguous, 128-byte rows (BK = 64
+//    bf16 / 32 f32) of eight 16-byte chunks XOR-swizzled by (row ^ row>>3) & 7:
+//    every MFMA fragment is one conflict-free ds_read_b128.  A K-contiguous
+//    source is staged with global_load_dwordx4 -> ds_write_b128; an M/N-contiguous
+//    (transposed) source is loaded as 4 k-rows x 16 B and transposed in registers
+//    before the LDS write, so all layouts share one MFMA inner loop.
+//  * two LDS buffers, the next K-tile's global loads issued before the current
+//    tile's MFMAs, one barrier per K-tile.
+//  * blockIdx is remapped so that consecutive tiles land on the same XCD (the
+//    dispatcher deals workgroups round-robin over the 8 XCDs, each with its own
+//    L2), then grouped 8 M-tiles at a time for operand reuse in that L2.
+#include "dtp_common.h"
+#include "dtp_api.h"
+
+namespace dtp {
+namespace gemm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kBM = 128, kBN = 128, kThreads = 256;
+constexpr int kChunks = 8;  // 16-byte chunks per 128-byte LDS row
+
+template <int DT>
+struct Ty {
+  static constexpr int ES = DT == DTP_DT_BF16 ? 2 : 4;  // element bytes
+  static constexpr int EPC = 16 / ES;                    // elements per 16-byte chunk
+  static constexpr int BK = 128 / ES;                    // K per tile (one LDS row)
+};
+
+DTP_DEV int swz(int row) { return (row ^ (row >> 3)) & 7; }
+DTP_DEV int slot(int row, int chunk) { return row * kChunks + (chunk ^ swz(row)); }
+
+DTP_DEV float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+DTP_DEV uint16_t f32_to_bf16(float f) {  // round to nearest even
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return uint16_t((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+template <int DT>
+DTP_DEV float load_elem(const char* p) {
+  if constexpr (DT == DTP_DT_BF16) return bf16_to_f32(*reinterpret_cast<const uint16_t*>(p));
+  else return *reinterpret_cast<const float*>(p);
+}
+
+// 16 bytes of row `r` (memory row), elements [c, c+EPC) of a matrix with `rows` rows,
+// `cols` columns and leading dimension `ld`; out-of-range elements read as 0.
+template <int DT>
+DTP_DEV uint4 load_chunk(const char* base, long long ld, int r, int c, int rows, int cols, bool vec) {
+  using T = Ty<DT>;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (r >= rows || c >= cols) return v;
+  const char* p = base + (static_cast<long long>(r) * ld + c) * T::ES;
+  if (vec && c + T::EPC <= cols) return *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int e = 0; e < T::EPC; ++e) {
+    if (c + e < cols) {
+      if constexpr (DT == DTP_DT_BF16) {
+        const uint32_t h = *reinterpret_cast<const uint16_t*>(p + e * 2);
+        w[e >> 1] |= h << ((e & 1) * 16);
+      } else {
+        w[e] = *reinterpret_cast<const uint32_t*>(p + e * 4);
+      }
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Staging registers of one operand tile (kBM or kBN rows x BK) for one thread.
+struct Stage {
+  uint4 v[4];
+};
+
+// Operand X(row, k), rows [row0, row0+128), k [k0, k0+BK).
+//   trans = 0: X(row,k) at base[row*ld + k]    (memory rows = operand rows)
+//   trans = 1: X(row,k) at base[k*ld + row]    (memory rows = k)
+template <int DT, bool TRANS>
+DTP_DEV void stage_load(Stage& s, const char* base, long long ld, int row0, int k0, int R, int K, bool vec, int tid) {
+  using T = Ty<DT>;
+  if constexpr (!TRANS) {
+    const int c = tid & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      s.v[i] = load_chunk<DT>(base, ld, row0 + r, k0 + c * T::EPC, R, K, vec);
+    }
+  } else {
+    constexpr int RC = kBM / T::EPC;  // row chunks per tile
+    const int mc = tid % RC, kq = tid / RC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s.v[i] = load_chunk<DT>(base, ld, k0 + 4 * kq + i, row0 + mc * T::EPC, K, R, vec);
+  }
+}
+
+template <int DT, bool TRANS>
+DTP_DEV void stage_store(const Stage& s, uint4* __restrict__ lds, int tid) {
+  using T = Ty<DT>;
+  if constexpr (!TRANS) {
+    const int c = tid & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds[slot((tid >> 3) + 32 * i, c)] = s.v[i];
+  } else if constexpr (DT == DTP_DT_F32) {
+    // 4 k-rows x 4 rows of floats -> for each row one 16-byte chunk (k = 4kq .. 4kq+3)
+    constexpr int RC = kBM / T::EPC;
+    const int mc = tid % RC, kq = tid / RC;
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&s.v[0]);
+    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&s.v[1]);
+    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&s.v[2]);
+    const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&s.v[3]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lds[slot(mc * 4 + e, kq)] = make_uint4(w0[e], w1[e], w2[e], w3[e]);
+  } else {
+    // bf16: 4 k-rows x 8 rows -> for each row 8 bytes (k = 4kq .. 4kq+3) = half a chunk
+    constexpr int RC = kBM / T::EPC;
+    const int mc = tid % RC, kq = tid / RC;
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&s.v[0]);
+    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&s.v[1]);
+    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&s.v[2]);
+    const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&s.v[3]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int sh = (e & 1) * 16, q = e >> 1;
+      const uint32_t lo = ((w0[q] >> sh) & 0xffffu) | (((w1[q] >> sh) & 0xffffu) << 16);
+      const uint32_t hi = ((w2[q] >> sh) & 0xffffu) | (((w3[q] >> sh) & 0xffffu) << 16);
+      uint2* dst = reinterpret_cast<uint2*>(lds + slot(mc * 8 + e, kq >> 1)) + (kq & 1);
+      *dst = make_uint2(lo, hi);
+    }
+  }
+}
+
+template <int DT, bool TA, bool TB>
+__global__ __launch_bounds__(kThreads) void gemm_kernel(DtpGemmArgs a) {
+  using T = Ty<DT>;
+  __shared__ uint4 lds[2][2][kBM * kChunks];  // [buffer][A|B][row*8 + chunk]: 64 KiB
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, lr = lane & 15, lg = lane >> 4;
+
+  // ---- tile decode: XCD-aware remap, then 8-row groups of M tiles ----
+  const int tm = (a.M + kBM - 1) / kBM, tn = (a.N + kBN - 1) / kBN;
+  int b = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  const int ks = b % a.splitk;
+  const int t = b / a.splitk;
+  const int group = t / (8 * tn), first_m = group * 8;
+  const int gsz = min(tm - first_m, 8);
+  const int pid_m = first_m + (t % (8 * tn)) % gsz;
+  const int pid_n = (t % (8 * tn)) / gsz;
+  const int m0 = pid_m * kBM, n0 = pid_n * kBN;
+
+  const int ktiles = (a.K + T::BK - 1) / T::BK;
+  const int kper = (ktiles + a.splitk - 1) / a.splitk;
+  const int kt0 = ks * kper, kt1 = min(ktiles, kt0 + kper);
+
+  const char* A = static_cast<const char*>(a.A);
+  const char* B = static_cast<const char*>(a.B);
+  const bool va = a.vec_a != 0, vb = a.vec_b != 0;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage sa, sb;
+  if (kt0 < kt1) {
+    stage_load<DT, TA>(sa, A, a.lda, m0, kt0 * T::BK, a.M, a.K, va, tid);
+    stage_load<DT, TB>(sb, B, a.ldb, n0, kt0 * T::BK, a.N, a.K, vb, tid);
+    stage_store<DT, TA>(sa, lds[0][0], tid);
+    stage_store<DT, TB>(sb, lds[0][1], tid);
+  }
+  __syncthreads();
+
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      stage_load<DT, TA>(sa, A, a.lda, m0, (kt + 1) * T::BK, a.M, a.K, va, tid);
+      stage_load<DT, TB>(sb, B, a.ldb, n0, (kt + 1) * T::BK, a.N, a.K, vb, tid);
+    }
+    const uint4* la = lds[buf][0];
+    const uint4* lb = lds[buf][1];
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      uint4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = la[slot(wm * 64 + 16 * i + lr, 4 * kc + lg)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = lb[slot(wn * 64 + 16 * j + lr, 4 * kc + lg)];
+      if constexpr (DT == DTP_DT_BF16) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                                __builtin_bit_cast(bf16x8, fb[j]), acc[i][j], 0, 0, 0);
+      } else {
+        // lane group lg supplies k = 4*(4kc+lg) + s at step s, for A and B alike
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float av = __uint_as_float(s == 0 ? fa[i].x : s == 1 ? fa[i].y : s == 2 ? fa[i].z : fa[i].w);
+              const float bv = __uint_as_float(s == 0 ? fb[j].x : s == 1 ? fb[j].y : s == 2 ? fb[j].z : fb[j].w);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
+            }
+      }
+    }
+    if (more) {
+      stage_store<DT, TA>(sa, lds[buf ^ 1][0], tid);
+      stage_store<DT, TB>(sb, lds[buf ^ 1][1], tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: element (m, n) = acc[i][j][r], m = .. + 4*lg + r, n = .. + lr ----
+  char* C = static_cast<char*>(a.C);
+  const char* aux = static_cast<const char*>(a.aux);
+  const bool first_split = ks == 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + 16 * j + lr;
+    if (n >= a.N) continue;
+    const float bias = (a.bias && first_split) ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + 16 * i + 4 * lg + r;
+        if (m >= a.M) continue;
+        float v = a.alpha * acc[i][j][r] + bias;
+        if (aux) v *= leaky_grad_from_out(load_elem<DT>(aux + (static_cast<long long>(m) * a.ldaux + n) * Ty<DT>::ES),
+                                          a.slope);
+        if (a.act) v = leaky(v, a.slope);
+        const long long off = static_cast<long long>(m) * a.ldc + n;
+        if (a.out_dtype == DTP_DT_BF16) {
+          uint16_t* p = reinterpret_cast<uint16_t*>(C) + off;
+          if (a.accumulate) v += bf16_to_f32(*p);
+          *p = f32_to_bf16(v);
+        } else {
+          float* p = reinterpret_cast<float*>(C) + off;
+          if (a.splitk > 1) {
+            atomicAdd(p, v);
+          } else {
+            if (a.accumulate) v += *p;
+            *p = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// out[n] (+)= sum_m X[m*ld + n]: bias gradients.  64 columns x 4 row groups per block,
+// 1024 rows per block; partial sums of several row blocks meet in f32 atomics.
+template <int DT>
+__global__ __launch_bounds__(256) void colsum_kernel(const void* X, long long ld, int M, int N, float* out) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int r0 = blockIdx.y * 1024;
+  const int r1 = min(M, r0 + 1024);
+  float s = 0.f;
+  if (n < N) {
+    const char* base = static_cast<const char*>(X);
+    for (int m = r0 + g; m < r1; m += 4) s += load_elem<DT>(base + (static_cast<long long>(m) * ld + n) * Ty<DT>::ES);
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && n < N) {
+    s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    if (gridDim.y > 1) atomicAdd(out + n, s);
+    else out[n] += s;
+  }
+}
+
+}  // namespace gemm
+}  // namespace dtp
+
+using namespace dtp;
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
+  if (!in) return set_err(1, "dtp_gemm: null args");
+  DtpGemmArgs a = *in;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return set_err(1, "dtp_gemm: empty problem");
+  if (a.dtype != DTP_DT_F32 && a.dtype != DTP_DT_BF16) return set_err(1, "dtp_gemm: dtype must be f32 or bf16");
+  if (a.out_dtype != DTP_DT_F32 && a.out_dtype != DTP_DT_BF16) return set_err(1, "dtp_gemm: bad out dtype");
+  if (!a.A || !a.B || !a.C) return set_err(1, "dtp_gemm: null operand");
+  if (a.splitk < 1) a.splitk = 1;
+  if (a.splitk > 1 && (a.out_dtype != DTP_DT_F32 || a.act || a.aux))
+    return set_err(1, "dtp_gemm: split-K needs an f32 output and no activation epilogue");
+  const int epc = a.dtype == DTP_DT_BF16 ? 8 : 4;
+  a.vec_a = (a.lda % epc == 0) && aligned16(a.A);
+  a.vec_b = (a.ldb % epc == 0) && aligned16(a.B);
+  const int tm = (a.M + gemm::kBM - 1) / gemm::kBM, tn = (a.N + gemm::kBN - 1) / gemm::kBN;
+  const int bk = a.dtype == DTP_DT_BF16 ? 64 : 32;
+  const int ktiles = (a.K + bk - 1) / bk;
+  if (a.splitk > ktiles) a.splitk = ktiles;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.splitk > 1 && !a.accumulate) {  // atomics accumulate into C: clear it first
+    hipError_t e = hipMemset2DAsync(a.C, sizeof(float) * static_cast<size_t>(a.ldc), 0, sizeof(float) * a.N, a.M, s);
+    if (e != hipSuccess) return set_err(2, "dtp_gemm: clearing the split-K output failed");
+  }
+  const dim3 grid(tm * tn * a.splitk), block(gemm::kThreads);
+  const int key = (a.dtype == DTP_DT_BF16 ? 4 : 0) | (a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0);
+  switch (key) {
+    case 0: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_F32, false, false>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_F32, false, true>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_F32, true, false>), grid, block, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_F32, true, true>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_BF16, false, false>), grid, block, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_BF16, false, true>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_BF16, true, false>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm::gemm_kernel<DTP_DT_BF16, true, true>), grid, block, 0, s, a); break;
+  }
+  return check_launch("dtp_gemm");
+}
+
+extern "C" int dtp_colsum(const void* X, long long ld, int M, int N, int dtype, float* out, int accumulate,
+                          void* stream) {
+  if (!X || !out || M <= 0 || N <= 0) return set_err(1, "dtp_colsum: bad arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
+  const dim3 grid((N + 63) / 64, (M + 1023) / 1024), block(256);
+  if (dtype == DTP_DT_BF16)
+    hipLaunchKernelGGL((gemm::colsum_kernel<DTP_DT_BF16>), grid, block, 0, s, X, ld, M, N, out);
+  else
+    hipLaunchKernelGGL((gemm::colsum_kernel<DTP_DT_F32>), grid, block, 0, s, X, ld, M, N, out);
+  return check_launch("dtp_colsum");
+}

@@ -199,5 +199,6 @@ extern "C" int dtp_struct_sizes(int* out) {
   out[2] = (int)sizeof(DtpTrainArgs);
   out[3] = (int)sizeof(DtpStageArgs);
   out[4] = (int)sizeof(DtpOptArgs);
-  return 5;
+  out[5] = (int)sizeof(DtpGemmArgs);
+  return 6;
 }

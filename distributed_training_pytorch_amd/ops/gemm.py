@@ -1,0 +1,176 @@
+"""MFMA GEMM with fused Linear epilogues (``csrc/gemm.hip``) and the wide-MLP op built on it.
+
+The toy model's 10-wide layers run inside the fused train-step kernel
+(``ops/mlp.py``); any wider MLP -- ``models/wide.py`` -- runs its Linear layers
+through this LDS-tiled MFMA GEMM instead of hipBLASLt:
+
+* forward    ``h' = LeakyReLU(h W^T + b)``       bias + activation in the epilogue;
+* grad input ``dz' = (dz W) * LeakyReLU'(h)``    activation gradient in the epilogue;
+* grad W     ``dW = dz^T h``                     transposed operands staged through
+  registers, split-K over blocks when the output has too few tiles;
+* grad b     ``db = sum_m dz``                   column-sum kernel.
+
+Replaces the reference's cuBLAS ``addmm``/``mm`` + ATen ``leaky_relu(_backward)``
+/ ``sum`` kernels (``toy_model_and_data.py:12-25``).
+On CPU tensors every function runs the PyTorch reference of the same math (the
+gloo test paths); on a GPU the HIP kernels are required.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native as nat
+
+_DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16}
+_BM = 128
+
+
+def _ld(t: torch.Tensor, name: str) -> int:
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D, got {tuple(t.shape)}")
+    if t.stride(1) != 1 and t.shape[1] > 1:
+        raise ValueError(f"{name} needs a unit-stride last dimension (got strides {t.stride()})")
+    return max(t.stride(0), 1) if t.shape[0] > 1 else max(t.shape[1], 1)
+
+
+def _ref(a, b, trans_a, trans_b, bias, aux, act, slope, alpha):
+    A = (a.t() if trans_a else a).float()
+    B = (b.t() if trans_b else b).float()  # [N, K]
+    r = alpha * (A @ B.t())
+    if bias is not None:
+        r = r + bias.float()
+    if aux is not None:
+        r = r * torch.where(aux.float() > 0, 1.0, slope)
+    if act:
+        r = torch.nn.functional.leaky_relu(r, slope)
+    return r
+
+
+def _auto_splitk(M: int, N: int, K: int, dtype: torch.dtype) -> int:
+    tiles = math.ceil(M / _BM) * math.ceil(N / _BM)
+    ktiles = math.ceil(K / (64 if dtype == torch.bfloat16 else 32))
+    if tiles >= 128 or ktiles < 8:
+        return 1
+    return max(1, min(256 // tiles, ktiles // 4))
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
+         out: torch.Tensor | None = None, bias: torch.Tensor | None = None, aux: torch.Tensor | None = None,
+         act: bool = False, slope: float = 0.01, accumulate: bool = False, alpha: float = 1.0,
+         splitk: int | None = None, out_dtype: torch.dtype | None = None) -> torch.Tensor:
+    """C[M,N] (+)= epilogue(alpha * A(m,k) B(n,k)).
+
+    ``a`` is [M,K] (or [K,M] with ``trans_a``); ``b`` is [N,K] (or [K,N] with ``trans_b``).
+    Epilogue order: + bias[n], * LeakyReLU'(aux[m,n]), LeakyReLU, (+ old C), cast.
+    """
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm: inner dimensions differ ({K} vs {Kb})")
+    if a.dtype != b.dtype or a.dtype not in _DT:
+        raise ValueError(f"gemm: operands must share dtype float32 or bfloat16 (got {a.dtype}, {b.dtype})")
+    out_dtype = out_dtype or (out.dtype if out is not None else a.dtype)
+    if out is None:
+        out = (torch.zeros if accumulate else torch.empty)(M, N, dtype=out_dtype, device=a.device)
+    if out.shape != (M, N) or out.dtype != out_dtype:
+        raise ValueError(f"gemm: out must be [{M},{N}] {out_dtype}")
+    if aux is not None and (aux.shape != (M, N) or aux.dtype != a.dtype):
+        raise ValueError("gemm: aux must be [M,N] with the operands' dtype")
+    if a.device.type != "cuda" or not nat.native_enabled():
+        r = _ref(a, b, trans_a, trans_b, bias, aux, act, slope, alpha)
+        if accumulate:
+            r = r + out.float()
+        out.copy_(r.to(out_dtype))
+        return out
+    lib = nat.require(a.device)
+    if splitk is None:
+        splitk = _auto_splitk(M, N, K, a.dtype) if (out_dtype == torch.float32 and not act and aux is None) else 1
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
+        bias = bias.float().contiguous()
+    args = nat.GemmArgs()
+    args.A, args.B, args.C = nat.ptr(a), nat.ptr(b), nat.ptr(out)
+    args.bias = nat.ptr(bias)
+    args.aux = nat.ptr(aux)
+    args.lda, args.ldb, args.ldc = _ld(a, "a"), _ld(b, "b"), _ld(out, "out")
+    args.ldaux = _ld(aux, "aux") if aux is not None else 0
+    args.M, args.N, args.K = M, N, K
+    args.dtype, args.out_dtype = _DT[a.dtype], _DT[out_dtype]
+    args.trans_a, args.trans_b = int(trans_a), int(trans_b)
+    args.act, args.accumulate, args.splitk = int(act), int(accumulate), int(splitk)
+    args.alpha, args.slope = float(alpha), float(slope)
+    nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
+    return out
+
+
+def colsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """out[n] (+)= sum_m x[m, n] in fp32 (bias gradients)."""
+    M, N = x.shape
+    if out is None:
+        out = torch.zeros(N, dtype=torch.float32, device=x.device)
+    if x.device.type != "cuda" or not nat.native_enabled():
+        s = x.float().sum(0)
+        out.copy_(out + s if accumulate else s)
+        return out
+    lib = nat.require(x.device)
+    nat.check(lib.dtp_colsum(nat.ptr(x), _ld(x, "x"), M, N, _DT[x.dtype], nat.ptr(out), int(accumulate),
+                             nat.stream_ptr()), "dtp_colsum")
+    return out
+
+
+class MLPFunction(torch.autograd.Function):
+    """y = L_{n-1}(... LeakyReLU(L_0(x)) ...) with every matmul on the MFMA GEMM.
+
+    ``compute_dtype`` bf16 = autocast-style mixed precision: fp32 master weights
+    cast once per forward, bf16 activations, fp32 accumulation and fp32 weight /
+    bias gradients; fp32 = exact-fp32 MFMA throughout.
+    """
+
+    @staticmethod
+    def forward(ctx, x, slope, compute_dtype, *params):
+        weights, biases = params[0::2], params[1::2]
+        L = len(weights)
+        ws = [w.detach().to(compute_dtype).contiguous() for w in weights]
+        h = x.detach().to(compute_dtype).contiguous()
+        hs = [h]
+        for l in range(L):
+            last = l == L - 1
+            h = gemm(h, ws[l], bias=biases[l].detach(), act=not last, slope=slope,
+                     out_dtype=torch.float32 if last else compute_dtype)
+            if not last:
+                hs.append(h)
+        ctx.save_for_backward(*hs, *ws)
+        ctx.L, ctx.slope, ctx.x_dtype = L, slope, x.dtype
+        ctx.x_needs = ctx.needs_input_grad[0]
+        return h
+
+    @staticmethod
+    def backward(ctx, gy):
+        L, slope = ctx.L, ctx.slope
+        saved = ctx.saved_tensors
+        hs, ws = saved[:L], saved[L:]
+        cd = ws[0].dtype
+        dz = gy.to(cd).contiguous()
+        gW: list[torch.Tensor | None] = [None] * L
+        gb: list[torch.Tensor | None] = [None] * L
+        dx = None
+        for l in range(L - 1, -1, -1):
+            gW[l] = gemm(dz, hs[l], trans_a=True, trans_b=True, out_dtype=torch.float32)
+            gb[l] = colsum(dz)
+            if l > 0:
+                dz = gemm(dz, ws[l], trans_b=True, aux=hs[l], slope=slope, out_dtype=cd)
+            elif ctx.x_needs:
+                dx = gemm(dz, ws[0], trans_b=True, out_dtype=torch.float32).to(ctx.x_dtype)
+        grads = []
+        for l in range(L):
+            grads += [gW[l], gb[l]]
+        return (dx, None, None, *grads)
+
+
+def mlp(x: torch.Tensor, weights: list[torch.Tensor], biases: list[torch.Tensor], slope: float = 0.01,
+        compute_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    params = []
+    for w, b in zip(weights, biases):
+        params += [w, b]
+    return MLPFunction.apply(x, slope, compute_dtype, *params)

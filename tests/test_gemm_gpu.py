@@ -1,0 +1,111 @@
+"""MFMA GEMM (csrc/gemm.hip) against plain PyTorch fp32 references, every operand
+layout, both input dtypes, every epilogue, split-K; the wide-MLP op against autograd."""
+import pytest
+import torch
+
+from distributed_training_pytorch_amd.models.wide import WideMLP
+from distributed_training_pytorch_amd.ops.gemm import colsum, gemm
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _ref(a, b, ta, tb):
+    A = (a.t() if ta else a).double()
+    B = (b.t() if tb else b).double()
+    return (A @ B.t()).float()
+
+
+def _ops(M, N, K, ta, tb, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(*((K, M) if ta else (M, K)), generator=g).to(DEV, dtype)
+    b = torch.randn(*((K, N) if tb else (N, K)), generator=g).to(DEV, dtype)
+    return a, b
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape", [(128, 128, 64), (200, 72, 40), (257, 300, 129), (64, 1, 10), (1, 37, 2)])
+def test_gemm_f32_layouts(ta, tb, shape):
+    M, N, K = shape
+    a, b = _ops(M, N, K, ta, tb, torch.float32)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, splitk=1)
+    torch.testing.assert_close(c, _ref(a, b, ta, tb), rtol=1e-5, atol=1e-4 * K ** 0.5)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape", [(256, 256, 256), (200, 72, 40), (130, 520, 136), (64, 3, 8)])
+def test_gemm_bf16_layouts(ta, tb, shape):
+    M, N, K = shape
+    a, b = _ops(M, N, K, ta, tb, torch.bfloat16)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1)
+    # inputs are exact bf16 values: only the f32 accumulation order differs
+    torch.testing.assert_close(c, _ref(a, b, ta, tb), rtol=1e-4, atol=1e-3 * K ** 0.5)
+    cb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, splitk=1)
+    torch.testing.assert_close(cb.float(), c, rtol=1e-2, atol=1e-2)
+
+
+def test_gemm_epilogues():
+    M, N, K = 300, 200, 96
+    a, b = _ops(M, N, K, False, False, torch.float32, 1)
+    bias = torch.randn(N, device=DEV)
+    aux = torch.randn(M, N, device=DEV)
+    base = _ref(a, b, False, False)
+    c = gemm(a, b, bias=bias, act=True, slope=0.1, alpha=0.5)
+    torch.testing.assert_close(c, torch.nn.functional.leaky_relu(0.5 * base + bias, 0.1), rtol=1e-5, atol=1e-4)
+    c = gemm(a, b, aux=aux, slope=0.01)
+    torch.testing.assert_close(c, base * torch.where(aux > 0, 1.0, 0.01), rtol=1e-5, atol=1e-4)
+    old = torch.randn(M, N, device=DEV)
+    c = gemm(a, b, out=old.clone(), accumulate=True)
+    torch.testing.assert_close(c, base + old, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("splitk", [2, 5])
+def test_gemm_splitk(splitk):
+    M, N, K = 96, 130, 1000
+    a, b = _ops(M, N, K, True, True, torch.float32, 2)
+    c = gemm(a, b, trans_a=True, trans_b=True, splitk=splitk)
+    torch.testing.assert_close(c, _ref(a, b, True, True), rtol=1e-5, atol=1e-3)
+    bias = torch.randn(N, device=DEV)
+    c = gemm(a, b, trans_a=True, trans_b=True, splitk=splitk, bias=bias)
+    torch.testing.assert_close(c, _ref(a, b, True, True) + bias, rtol=1e-5, atol=1e-3)
+
+
+def test_gemm_strided_views():
+    big = torch.randn(300, 512, device=DEV)
+    a = big[:, 8:8 + 96]      # ld 512, offset: 16-byte aligned views stay vectorised
+    b = torch.randn(64, 96, device=DEV)
+    torch.testing.assert_close(gemm(a, b), _ref(a, b, False, False), rtol=1e-5, atol=1e-4)
+    a2 = big[:, 3:3 + 96]     # misaligned: per-element fallback
+    torch.testing.assert_close(gemm(a2, b), _ref(a2, b, False, False), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M", [5, 1000, 3000])
+def test_colsum(M):
+    x = torch.randn(M, 77, device=DEV)
+    torch.testing.assert_close(colsum(x), x.sum(0), rtol=1e-5, atol=1e-4)
+    out = torch.ones(77, device=DEV)
+    torch.testing.assert_close(colsum(x.bfloat16(), out=out, accumulate=True), 1 + x.bfloat16().float().sum(0),
+                               rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 3e-2)])
+def test_wide_mlp_grads_vs_autograd(dtype, tol):
+    torch.manual_seed(0)
+    m = WideMLP((2, 256, 192, 256, 1), compute_dtype=dtype).to(DEV)
+    x = torch.randn(384, 2, device=DEV, requires_grad=True)
+    y = torch.randn(384, 1, device=DEV)
+    out = m(x)
+    loss = torch.nn.functional.mse_loss(out, y)
+    loss.backward()
+    got = [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
+    m.zero_grad()
+    x.grad = None
+    ref_out = m.reference_forward(x)
+    torch.testing.assert_close(out, ref_out, rtol=tol, atol=tol)
+    torch.nn.functional.mse_loss(ref_out, y).backward()
+    ref = [p.grad for p in m.parameters()] + [x.grad]
+    for g, r in zip(got, ref):
+        scale = r.abs().max().clamp_min(1e-6)
+        assert ((g - r).abs().max() / scale) < tol * 5, (g - r).abs().max() / scale
