@@ -73,6 +73,7 @@ class TrainArgs(ctypes.Structure):
         ("status", c_void_p),
         ("peers", c_void_p),
         ("epoch", c_void_p),
+        ("wsp", c_void_p),
         ("loss_log_cap", c_int),
         ("n_models", c_int),
         ("n_steps", c_int),
@@ -162,6 +163,7 @@ def _declare(lib):
         "dtp_runtime_last_error": (ctypes.c_char_p, []),
         "dtp_mlp_supported": (c_int, [c_int] * 5),
         "dtp_mlp_param_count": (c_int, [c_int] * 4),
+        "dtp_mlp_workspace_floats": (c_int, [c_int] * 4),
         "dtp_mlp_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),

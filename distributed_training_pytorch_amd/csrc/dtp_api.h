@@ -36,6 +36,7 @@ struct DtpTrainArgs {
   int* status;          // [16] error / timeout words (xGMI mode), nullable
   float* const* peers;  // MODE_XGMI_*: [world] device pointers of every rank's receive buffer
   unsigned* epoch;      // MODE_XGMI_*: [n_models] exchange epoch counters (device)
+  float* wsp;           // [n_models][dtp_mlp_workspace_floats] scalar-weight workspace (scratch)
   int loss_log_cap;
   int n_models;
   int n_steps;
@@ -50,6 +51,7 @@ int dtp_version(void);
 const char* dtp_last_error(void);
 int dtp_mlp_supported(int in, int h, int nl, int out, int final_act);
 int dtp_mlp_param_count(int in, int h, int nl, int out);
+int dtp_mlp_workspace_floats(int in, int h, int nl, int out);
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream);
 int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream);
 

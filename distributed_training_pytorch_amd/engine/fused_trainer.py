@@ -93,6 +93,12 @@ class FusedTrainer:
             nat.require(self.device)
             if not spec.native_supported():
                 raise NotImplementedError(f"no fused kernel for {spec}")
+            lib = nat.require(self.device)
+            ws = lib.dtp_mlp_workspace_floats(spec.in_features, spec.hidden, spec.n_layers, spec.out_features)
+            if ws <= 0:
+                raise NotImplementedError(f"no fused train kernel for {spec}")
+            # scalar-weight workspace of the fused step (csrc/mlp_scalar.h), scratch
+            self.wsp = torch.zeros(n_models * ws, dtype=torch.float32, device=dev)
         if self.comm == "xgmi":
             self._setup_xgmi()
 
@@ -190,7 +196,7 @@ class FusedTrainer:
             nat.ptr(self.X), nat.ptr(self.Y), nat.ptr(idx), nat.ptr(self.params), nat.ptr(self.m), nat.ptr(self.v),
             nat.ptr(self.step_ctr), nat.ptr(self.comm_buf), nat.ptr(self.loss_log),
             nat.ptr(xg.status) if xg else None, nat.ptr(xg.peer_table) if xg else None,
-            nat.ptr(xg.epoch) if xg else None,
+            nat.ptr(xg.epoch) if xg else None, nat.ptr(getattr(self, "wsp", None)),
             self.loss_log.shape[0], self.n_models, n_steps,
             nat.LOSS_CE if self.cfg.loss == "ce" else nat.LOSS_MSE,
             int(self.cfg.cache_data), self.cfg.xgmi_timeout_us, smp,

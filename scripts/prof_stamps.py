@@ -42,7 +42,7 @@ def main():
             s = st[0, it]
             d = {NAMES[k]: int(s[k] - s[k - 1]) for k in range(1, 8)}
             d["total_step"] = int(st[0, it, 7] - st[0, it, 0]) if it else 0
-            d["wave_bwd_end_rel"] = [int(st[0, it, 8 + w] - st[0, it, 0]) for w in range(8)]
+            d["wave_bwd_end_rel"] = [int(st[0, it, 8 + w] - st[0, it, 0]) for w in range(4)]
             fl = [int(st[0, it, 16 + l]) for l in range(8) if int(st[0, it, 16 + l])]
             d["fwd_layers"] = [int(b - a) for a, b in zip([int(s[1])] + fl[:-1], fl)]
             bl = [int(st[0, it, 24 + l]) for l in range(8) if int(st[0, it, 24 + l])][::-1]

@@ -90,22 +90,35 @@ def test_colsum(M):
                                rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 3e-2)])
+def _emulated_forward(m, x, dtype):
+    """The same graph in fp32 autograd, operands rounded to `dtype` where the kernels round them."""
+    q = (lambda t: t.to(dtype).float()) if dtype != torch.float32 else (lambda t: t)
+    lins = m.linears()
+    h = q(x)
+    for l, lin in enumerate(lins):
+        z = h @ q(lin.weight).t() + lin.bias
+        if l < len(lins) - 1:
+            h = q(torch.nn.functional.leaky_relu(z, m.slope))
+        else:
+            h = z
+    return h
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
 def test_wide_mlp_grads_vs_autograd(dtype, tol):
     torch.manual_seed(0)
     m = WideMLP((2, 256, 192, 256, 1), compute_dtype=dtype).to(DEV)
     x = torch.randn(384, 2, device=DEV, requires_grad=True)
     y = torch.randn(384, 1, device=DEV)
     out = m(x)
-    loss = torch.nn.functional.mse_loss(out, y)
-    loss.backward()
+    torch.nn.functional.mse_loss(out, y).backward()
     got = [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
     m.zero_grad()
     x.grad = None
-    ref_out = m.reference_forward(x)
+    ref_out = _emulated_forward(m, x, dtype)
     torch.testing.assert_close(out, ref_out, rtol=tol, atol=tol)
     torch.nn.functional.mse_loss(ref_out, y).backward()
     ref = [p.grad for p in m.parameters()] + [x.grad]
     for g, r in zip(got, ref):
-        scale = r.abs().max().clamp_min(1e-6)
-        assert ((g - r).abs().max() / scale) < tol * 5, (g - r).abs().max() / scale
+        rel = (g - r).abs().max() / r.abs().max().clamp_min(1e-6)
+        assert rel < tol, rel
