@@ -20,15 +20,19 @@
 
 namespace dtp {
 
-constexpr int kDataCache = 4096;  // floats of dataset that may be staged in LDS
+// floats of dataset staged in LDS: the whole weak-scaling dataset of an 8-GPU
+// node (n = 512 x 8 samples x (2 inputs + 1 target)) stays on-chip
+constexpr int kDataCache = 12288;
 constexpr int kPermCap = 2048;    // per-rank epoch permutation kept in LDS
 constexpr int kWaves = kBlock / kWave;
 
 template <class S>
 struct TrainSmem {
-  // per wave: [packed first/last tile | hidden parity 0 | hidden parity 1] x (dz rows, h rows);
-  // reused for the cross-wave dW tile reduction
-  float stage[kWaves][3][2 * kStgArr];
+  // per wave: [packed first/last tile | hidden layer] x (dz rows, h rows) -- one hidden
+  // buffer suffices: a wave's LDS ops execute in order, so layer l-1's staging
+  // writes land after layer l's operand reads were issued; reused for the
+  // cross-wave dW tile reduction
+  float stage[kWaves][2][2 * kStgArr];
   float data[kDataCache];
   int perm[kPermCap];
 };
@@ -57,7 +61,7 @@ template <class S, int MODE, bool PROF = false>
 __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT;
-  static_assert(kWaves * NT * 256 <= kWaves * 3 * 2 * kStgArr, "reduction tiles must fit in the staging area");
+  static_assert(kWaves * NT * 256 <= kWaves * 2 * 2 * kStgArr, "reduction tiles must fit in the staging area");
   __shared__ __align__(16) TrainSmem<S> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
@@ -207,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
         constexpr int l = NL - 1 - decltype(RC)::value;
         constexpr int I = S::din(l), O = S::dout(l);
         constexpr bool packed = SC::PACK && (l == 0 || l == NL - 1);
-        float* stg = packed ? stg_pack : &sm.stage[wave][1 + (l & 1)][0];
+        float* stg = packed ? stg_pack : &sm.stage[wave][1][0];
         float* dzb = stg;
         float* hb = stg + kStgArr;
         stage_cols<O>(dzb, lane, SC::rowoff(l), dz);

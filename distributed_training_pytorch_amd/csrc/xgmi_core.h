@@ -38,23 +38,8 @@ DTP_DEV unsigned long long load_granule_sys(const unsigned long long* p) {
   return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-DTP_DEV float poll_granule(const unsigned long long* p, unsigned epoch, unsigned long long deadline, bool& dead,
-                           int* status) {
-  for (;;) {
-    const unsigned long long x = load_granule_sys(p);
-    if ((unsigned)(x >> 32) == epoch) return __uint_as_float((unsigned)x);
-    if (dead) return 0.f;
-    if (__builtin_amdgcn_s_memrealtime() > deadline) {
-      dead = true;
-      if (status) {
-        atomicExch(&status[0], 1);
-        atomicExch(&status[1], (int)epoch);
-      }
-      return 0.f;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
+// largest world the in-kernel exchange serves (one node: 8 GPUs, 7 xGMI links each)
+constexpr int kXgmiMaxWorld = 8;
 
 // granules per (model, src rank) slot: P gradient values + 1 loss, 64-byte rounded
 DTP_HD int xgmi_slot_granules(int P) { return (P + 1 + 7) & ~7; }
@@ -76,28 +61,72 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
     }
     if (tid == 0) store_granule_sys(dst + P, pack_granule(epoch, loss));
   }
-  // consume every rank's slot from our local buffer, summing in rank order
+  // consume every rank's slot from our local buffer: every granule this thread
+  // needs (W x (NPT + loss)) is requested at once and only the missing ones are
+  // re-polled, so an exchange costs ONE uncached round trip once the data is
+  // there, not W sequential ones; then sum in rank order 0..W-1 (bitwise
+  // identical on every rank)
   const unsigned long long* mine = reinterpret_cast<const unsigned long long*>(a.peers[R]);
   const unsigned long long deadline =
       __builtin_amdgcn_s_memrealtime() + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
   // sticky failure: once any exchange of this rank timed out, later ones do not
   // wait again (a persistent launch must not multiply the timeout by its steps)
   bool dead = a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
-  float acc[NPT];
+  constexpr int NG = NPT + 1;  // + the loss granule (thread 0)
+  float val[kXgmiMaxWorld][NG];
+  static_assert(kXgmiMaxWorld * NG <= 64, "pending mask holds every (rank, granule) pair");
+  uint64_t pending = 0ull;  // bit r*NG + k: granule (r, k) still missing
 #pragma unroll
-  for (int k = 0; k < NPT; ++k) acc[k] = 0.f;
-  float lacc = 0.f;
-  for (int r = 0; r < W; ++r) {
-    const unsigned long long* src = mine + (base + r) * slot;
+  for (int r = 0; r < kXgmiMaxWorld; ++r) {
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int p = tid + k * NTHREADS;
-      if (p < P) acc[k] += poll_granule(src + p, epoch, deadline, dead, a.status);
+    for (int k = 0; k < NG; ++k) {
+      val[r][k] = 0.f;
+      const int p = k < NPT ? tid + k * NTHREADS : P;
+      const bool mine_to_read = r < W && (k < NPT ? p < P : tid == 0);
+      if (mine_to_read) pending |= 1ull << (r * NG + k);
     }
-    if (tid == 0) lacc += poll_granule(src + P, epoch, deadline, dead, a.status);
+  }
+  while (pending && !dead) {
+    unsigned long long x[kXgmiMaxWorld][NG];
+#pragma unroll
+    for (int r = 0; r < kXgmiMaxWorld; ++r) {
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int p = k < NPT ? tid + k * NTHREADS : P;
+        x[r][k] = (pending >> (r * NG + k)) & 1ull ? load_granule_sys(mine + (base + r) * slot + p) : 0ull;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kXgmiMaxWorld; ++r) {
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        if (((pending >> (r * NG + k)) & 1ull) && (unsigned)(x[r][k] >> 32) == epoch) {
+          val[r][k] = __uint_as_float((unsigned)x[r][k]);
+          pending &= ~(1ull << (r * NG + k));
+        }
+      }
+    }
+    if (!pending) break;
+    if (__builtin_amdgcn_s_memrealtime() > deadline) {
+      dead = true;
+      if (a.status) {
+        atomicExch(&a.status[0], 1);
+        atomicExch(&a.status[1], (int)epoch);
+      }
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float lacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < kXgmiMaxWorld; ++r) acc += val[r][k];  // absent ranks contribute +0.0f
+    g[k] = acc;
   }
 #pragma unroll
-  for (int k = 0; k < NPT; ++k) g[k] = acc[k];
+  for (int r = 0; r < kXgmiMaxWorld; ++r) lacc += val[r][NPT];
   return lacc;
 }
 

@@ -115,6 +115,8 @@ class FusedTrainer:
             return "xgmi" if self.world <= 8 else "rccl"
         if c not in ("rccl", "xgmi", "host"):
             raise ValueError(f"comm {c!r} not valid for a GPU run with world={self.world}")
+        if c == "xgmi" and self.world > 8:
+            raise ValueError("comm='xgmi' is the single-node (<= 8 GPU) in-kernel exchange; use 'rccl' beyond")
         return c
 
     def _setup_xgmi(self):

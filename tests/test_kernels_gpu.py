@@ -122,6 +122,26 @@ def test_fused_trainer_matches_reference(launch):
     tr.close()
 
 
+@pytest.mark.parametrize("n,cache", [(4096, True), (4096, False), (8192, True)])
+def test_fused_trainer_large_dataset(n, cache):
+    """The 8-GPU weak-scaling dataset (n = 4096) stays in LDS; beyond it the kernel
+    gathers from global memory -- same numbers either way."""
+    ds = ToyData(n=n, seed=4)
+    X, Y = ds.device_tensors(DEV)
+    geom = SamplerGeometry(n=n, batch=256, seed=2)
+    init = [_params(TOY_SPEC, 30 + i, 0.4) for i in range(2)]
+    cfg = OptimConfig(lr=1e-2)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, cfg, EngineConfig(steps_per_launch=5, cache_data=cache),
+                      init_params=init)
+    steps = 10
+    tr.train(steps)
+    tr.synchronize()
+    ref_p, ref_l = _ref_train(TOY_SPEC, torch.stack(init), X, Y, geom, steps, cfg)
+    torch.testing.assert_close(tr.losses(0, steps), ref_l, rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(tr.params, ref_p, rtol=1e-3, atol=2e-5)
+    tr.close()
+
+
 def test_fused_trainer_torch_sampler_order():
     ds = ToyData(seed=3)
     X, Y = ds.device_tensors(DEV)
