@@ -185,6 +185,7 @@ def _declare(lib):
         "dtp_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
         "dtp_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
         "dtp_stream_sync": (c_int, [c_void_p]),
+        "dtp_device_sync_check": (c_int, []),
         "dtp_graph_capture_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                             P(c_void_p)]),
         "dtp_graph_launch": (c_int, [c_void_p, c_void_p]),
@@ -245,11 +246,21 @@ def require(device: torch.device | None = None):
         raise NativeUnavailable(f"native HIP kernels are required on {device or 'GPU'}: {e}") from e
 
 
+def debug_enabled() -> bool:
+    """DTP_DEBUG=1: synchronise + error-check after every native call, poison fresh outputs."""
+    return os.environ.get("DTP_DEBUG", "0") == "1"
+
+
 def check(rc: int, what: str):
     if rc != 0:
         lib = load()
         msg = (lib.dtp_last_error() or b"").decode() or (lib.dtp_runtime_last_error() or b"").decode()
         raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
+    if debug_enabled():
+        lib = load()
+        if lib.dtp_device_sync_check() != 0:
+            msg = (lib.dtp_runtime_last_error() or b"").decode()
+            raise RuntimeError(f"{what}: device fault surfaced by DTP_DEBUG sync: {msg}")
 
 
 def stream_ptr(stream: torch.cuda.Stream | None = None) -> int:

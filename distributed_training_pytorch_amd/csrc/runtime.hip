@@ -140,6 +140,14 @@ int dtp_stream_sync(void* stream) {
   return 0;
 }
 
+// debug mode (DTP_DEBUG=1): drain the device after a native call and surface any
+// asynchronous kernel fault at the call that caused it
+int dtp_device_sync_check(void) {
+  RT_CHECK(hipDeviceSynchronize());
+  RT_CHECK(hipGetLastError());
+  return 0;
+}
+
 // ---- graph executor --------------------------------------------------------
 int dtp_graph_capture_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, int launches,
                             void* stream, void** handle_out) {

@@ -32,6 +32,8 @@ from ..parallel import comm_util
 from ..runtime import bootstrap, checkpoint
 from ..runtime.errors import FaultInjector, check_replicas
 from ..utils.logging import MetricLogger, rank_print
+from ..utils.profiling import PhaseTimer
+from ..utils.profiling import enabled as trace_enabled
 
 
 def setup(config, launcher: str | None = None, gpus_per_proc: int = 1):
@@ -144,14 +146,17 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
         pbar.update(start)
     it = start
     chunk = max(1, min(config.log_every, config.steps_per_launch))
+    timer = PhaseTimer(device)
     t0 = time.perf_counter()
     while it < config.iters:
         n = min(chunk, config.iters - it)
         if faults.armed() and it <= config.fail_at_iter < it + n:
             n = config.fail_at_iter - it
         if n > 0:
-            tr.train(n)
-            ls = tr.losses(it, it + n)  # one host sync per chunk
+            with timer.phase("train_chunk"):
+                tr.train(n)
+            with timer.phase("loss_readback"):
+                ls = tr.losses(it, it + n)  # one host sync per chunk
             for k in range(n):
                 logger.log({"loss/lossX": ls[k, 0].item()}, step=it + k, commit=False)
                 logger.log({"loss/lossY": ls[k, 1].item()}, step=it + k)
@@ -173,7 +178,8 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
     final = tr.losses(it - 1, it)[0].tolist() if it > 0 else [float("nan")] * 2
     samples = geom.batch * (it - start) * world
     tr.close()
-    return {"final_loss": final, "iters": it, "samples_per_s": samples / max(dt, 1e-9), "engine": "fused"}
+    return {"final_loss": final, "iters": it, "samples_per_s": samples / max(dt, 1e-9), "engine": "fused",
+            **({"phases": timer.summary()} if trace_enabled() else {})}
 
 
 # ----------------------------------------------------------------------------- module engine
@@ -193,23 +199,29 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     opt = FlatOptimizer(bank.flat, bank.flat_grad, _optim(config))
     lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else torch.nn.MSELoss()
     pbar = _progress(rank, config.iters, config)
+    timer = PhaseTimer(device)
     t0 = time.perf_counter()
     lbuf = torch.zeros(2, device=device)
     for it in range(config.iters):
         faults.check(it)
-        idx = idx_stream.indices(it) if idx_stream is not None else geom.indices(it)
-        idx_t = torch.tensor(idx, device=device)
-        x, y = X[idx_t], Y[idx_t]
-        if config.loss == "ce":
-            y = y.view(-1).long()
+        with timer.phase("data"):
+            idx = idx_stream.indices(it) if idx_stream is not None else geom.indices(it)
+            idx_t = torch.tensor(idx, device=device)
+            x, y = X[idx_t], Y[idx_t]
+            if config.loss == "ce":
+                y = y.view(-1).long()
         bank.zero_grad()
-        ox, oy = ddp(x)
-        lx, ly = lossf(ox, y), lossf(oy, y)
-        (lx + ly).backward()  # independent models: one backward, one bucketed all-reduce
-        opt.step()
-        lbuf[0], lbuf[1] = lx.detach(), ly.detach()
-        comm_util.all_reduce_(lbuf)
-        lbuf.mul_(1.0 / world)
+        with timer.phase("forward"):
+            ox, oy = ddp(x)
+            lx, ly = lossf(ox, y), lossf(oy, y)
+        with timer.phase("backward+allreduce"):
+            (lx + ly).backward()  # independent models: one backward, one bucketed all-reduce
+        with timer.phase("optimizer"):
+            opt.step()
+        with timer.phase("loss_reduce"):
+            lbuf[0], lbuf[1] = lx.detach(), ly.detach()
+            comm_util.all_reduce_(lbuf)
+            lbuf.mul_(1.0 / world)
         if rank == 0:
             logger.log({"loss/lossX": lbuf[0].item()}, step=it, commit=False)
             logger.log({"loss/lossY": lbuf[1].item()}, step=it)
@@ -223,7 +235,8 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     if config.check_replicas:
         check_replicas(bank.flat)
     return {"final_loss": lbuf.tolist(), "iters": config.iters,
-            "samples_per_s": geom.batch * config.iters * world / max(dt, 1e-9), "engine": "module"}
+            "samples_per_s": geom.batch * config.iters * world / max(dt, 1e-9), "engine": "module",
+            **({"phases": timer.summary()} if trace_enabled() else {})}
 
 
 # ----------------------------------------------------------------------------- stock engine
@@ -233,10 +246,12 @@ def _train_stock(config, device, rank, world, logger, faults) -> dict:
     ds = _dataset(config, rank)
     loop = StockLoop(ds, device, batch=config.batch_size, seed=config.seed)
     pbar = _progress(rank, config.iters, config)
+    timer = PhaseTimer(device)
     t0 = time.perf_counter()
     for it in range(config.iters):
         faults.check(it)
-        loop.step()
+        with timer.phase("step"):
+            loop.step()
         if rank == 0:
             logger.log({"loss/lossX": loop.last[0]}, step=it, commit=False)
             logger.log({"loss/lossY": loop.last[1]}, step=it)
@@ -247,7 +262,8 @@ def _train_stock(config, device, rank, world, logger, faults) -> dict:
         pbar.close()
     loop.close()
     return {"final_loss": list(loop.last), "iters": config.iters,
-            "samples_per_s": loop.samples * world / max(dt, 1e-9), "engine": "stock"}
+            "samples_per_s": loop.samples * world / max(dt, 1e-9), "engine": "stock",
+            **({"phases": timer.summary()} if trace_enabled() else {})}
 
 
 def teardown():

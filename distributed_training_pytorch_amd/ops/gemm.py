@@ -74,6 +74,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     out_dtype = out_dtype or (out.dtype if out is not None else a.dtype)
     if out is None:
         out = (torch.zeros if accumulate else torch.empty)(M, N, dtype=out_dtype, device=a.device)
+        if not accumulate and nat.debug_enabled():
+            out.fill_(float("nan"))  # poisoned: any element the kernel fails to write shows up
     if out.shape != (M, N) or out.dtype != out_dtype:
         raise ValueError(f"gemm: out must be [{M},{N}] {out_dtype}")
     if aux is not None and (aux.shape != (M, N) or aux.dtype != a.dtype):

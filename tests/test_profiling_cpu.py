@@ -1,0 +1,44 @@
+"""Tracing helpers: no-op when disabled, phase accounting when enabled."""
+import torch
+
+from distributed_training_pytorch_amd.utils import profiling
+
+
+def test_trace_disabled_is_noop():
+    profiling.set_enabled(False)
+    t = profiling.PhaseTimer(torch.device("cpu"))
+    with profiling.trace_range("x"), t.phase("a"):
+        pass
+    assert t.summary() == {}
+
+
+def test_phase_timer_accumulates():
+    profiling.set_enabled(True, sync=False)
+    try:
+        t = profiling.PhaseTimer(torch.device("cpu"))
+        for _ in range(3):
+            with t.phase("fwd"):
+                torch.ones(10).sum()
+        with profiling.trace_range("outer"):
+            with t.phase("opt"):
+                pass
+        s = t.summary()
+        assert s["fwd"]["calls"] == 3 and s["opt"]["calls"] == 1 and s["fwd"]["s"] >= 0
+    finally:
+        profiling.set_enabled(False)
+
+
+def test_runner_reports_phases(tmp_path):
+    from distributed_training_pytorch_amd.engine import runner
+    from argument_parser import get_args
+    from distributed_training_pytorch_amd.runtime import bootstrap
+
+    profiling.set_enabled(True, sync=False)
+    try:
+        cfg = get_args(["--device", "cpu", "--backend", "gloo", "--iters", "3", "--engine", "module",
+                        "--no_progress", "--seed", "1", "--log_dir", str(tmp_path)])
+        env = bootstrap.detect()
+        summary = runner.train(cfg, env, torch.device("cpu"), 0, 1)
+        assert {"data", "forward", "backward+allreduce", "optimizer"} <= set(summary["phases"])
+    finally:
+        profiling.set_enabled(False)
