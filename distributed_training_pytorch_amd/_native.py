@@ -192,6 +192,8 @@ def _declare(lib):
         "dtp_graph_destroy": (c_int, [c_void_p]),
         "dtp_struct_sizes": (c_int, [P(c_int)]),
         "dtp_gemm": (c_int, [P(GemmArgs), c_void_p]),
+        "dtp_xgmi_allreduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, ctypes.c_uint, c_float,
+                                       c_void_p, c_int, c_void_p]),
         "dtp_colsum": (c_int, [c_void_p, c_longlong, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():

@@ -195,7 +195,9 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     torch.manual_seed(config.seed)
     out_f = 4 if config.loss == "ce" else 1
     bank = ModelBank(2, hidden=config.hidden, depth=config.depth, out_features=out_f).to(device)
-    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad)
+    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad,
+                  comm=config.comm if config.comm in ("auto", "rccl", "xgmi") else "rccl")
+    rank_print(rank, f"engine: module (FlatDDP over {ddp.comm})")
     opt = FlatOptimizer(bank.flat, bank.flat_grad, _optim(config))
     lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else torch.nn.MSELoss()
     pbar = _progress(rank, config.iters, config)

@@ -14,7 +14,11 @@ MI355X-first choices:
   start communication early, the rest large (default 64 MB -- 288 GB HBM makes
   memory irrelevant, and larger messages amortise the per-hop ring latency
   across the 7 point-to-point links);
-* ``comm="xgmi"`` routes small buckets through the one-shot peer all-reduce.
+* ``comm="auto"|"xgmi"`` routes buckets of up to 64 Ki floats through the
+  one-shot xGMI all-reduce (``parallel/xgmi.py: XgmiAllReduce``) on a side HIP
+  stream (one posted write per peer + one local read instead of a 2(W-1)-hop
+  ring), after a self-test against the process group; larger buckets, CPU/gloo
+  runs, more than 8 ranks or a failed self-test use RCCL (``comm="rccl"``).
 """
 from __future__ import annotations
 
@@ -28,16 +32,19 @@ from . import comm_util
 class FlatDDP(nn.Module):
     def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 64.0, first_bucket_mb: float = 1.0,
                  flat_params: torch.Tensor | None = None, flat_grad: torch.Tensor | None = None,
-                 broadcast: bool = True):
+                 broadcast: bool = True, comm: str = "auto"):
         super().__init__()
         self.module = module
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if comm not in ("auto", "rccl", "xgmi"):
+            raise ValueError(f"FlatDDP comm must be auto|rccl|xgmi, got {comm!r}")
         params = [p for p in module.parameters() if p.requires_grad]
         if flat_params is None or flat_grad is None:
             flat_params, flat_grad = self._flatten(params)
         self.flat_params = flat_params
         self.flat_grad = flat_grad
+        self._grad1d = flat_grad.view(-1)  # bucket spans index the flat ELEMENT space
         self._params = params
         # offsets of every param inside the flat grad
         base = flat_grad.data_ptr()
@@ -74,6 +81,55 @@ class FlatDDP(nn.Module):
             p.register_post_accumulate_grad_hook(self._hook)
         if broadcast and self.world > 1:
             comm_util.broadcast_(self.flat_params, 0, group)
+        self.comm = "rccl"
+        self._xgmi = None
+        self._side = None
+        self._xgmi_buckets: set[int] = set()
+        if comm in ("auto", "xgmi"):
+            self._setup_xgmi(strict=comm == "xgmi")
+
+    # ------------------------------------------------------------------ xGMI path
+    def _setup_xgmi(self, strict: bool):
+        from .xgmi import XgmiAllReduce
+
+        dev = self.flat_grad.device
+        why = ""
+        if self.world == 1:
+            why = "single rank"
+        elif dev.type != "cuda":
+            why = "needs GPU gradients"
+        elif self.world > 8:
+            why = "more than one node's worth of ranks"
+        small = [b for b, (lo, hi) in enumerate(self._spans) if hi - lo <= XgmiAllReduce.MAX_CAP]
+        if not why and not small:
+            why = "no bucket small enough"
+        if not why:
+            cap = max(self._spans[b][1] - self._spans[b][0] for b in small)
+            rank = dist.get_rank(self.group)
+            probe = torch.full((cap,), float(rank + 1), device=dev)
+            probe[::7] = 0.5 * (rank + 1)
+            expect = probe.clone()
+            comm_util.all_reduce_(expect, self.group)  # before anything that can fail: same collectives on all ranks
+            ok, ar = False, None
+            try:
+                ar = XgmiAllReduce(cap, dev, self.group)
+                ar.all_reduce_(probe)
+                torch.cuda.synchronize(dev)
+                ok = torch.equal(probe, expect) and not bool(ar.status[0].item())
+                why = "" if ok else "self-test mismatch"
+            except Exception as e:  # noqa: BLE001 - any mapping failure -> RCCL
+                why = f"setup failed: {e}"
+            flag = torch.tensor([1.0 if ok else 0.0], device=dev)
+            comm_util.all_reduce_(flag, self.group, op=dist.ReduceOp.MIN)  # every rank takes the same path
+            if flag.item() == 1.0:
+                self._xgmi, self._side, self.comm = ar, torch.cuda.Stream(dev), "xgmi"
+                self._xgmi_buckets = set(small)
+                return
+            if ar is not None:
+                ar.close()
+            why = why or "self-test failed on another rank"
+        if strict and self.world > 1:
+            raise RuntimeError(f"FlatDDP comm='xgmi' unavailable: {why}")
 
     @staticmethod
     def _flatten(params):
@@ -109,8 +165,15 @@ class FlatDDP(nn.Module):
         if self.world == 1:
             return
         lo, hi = self._spans[b]
-        view = self.flat_grad[lo:hi]
-        if dist.get_backend(self.group) == "nccl":
+        view = self._grad1d[lo:hi]
+        if b in self._xgmi_buckets:
+            # grads of this bucket are final on the current (backward) stream: reduce
+            # them on the side stream while the backward continues
+            self._side.wait_stream(torch.cuda.current_stream(view.device))
+            with torch.cuda.stream(self._side):
+                self._xgmi.all_reduce_(view)
+            self._works.append(("xgmi", view))
+        elif dist.get_backend(self.group) == "nccl":
             self._works.append((dist.all_reduce(view, group=self.group, async_op=True), view))
         else:
             comm_util.all_reduce_(view, self.group)
@@ -124,7 +187,9 @@ class FlatDDP(nn.Module):
             if not done:
                 self._reduce_bucket(b)
         for w, view in self._works:
-            if w is not None:
+            if w == "xgmi":
+                torch.cuda.current_stream(view.device).wait_stream(self._side)
+            elif w is not None:
                 w.wait()
         if self.world > 1:
             self.flat_grad.mul_(1.0 / self.world)
@@ -133,3 +198,8 @@ class FlatDDP(nn.Module):
 
     def zero_grad(self):
         self.flat_grad.zero_()
+
+    def check_comm(self):
+        """Raise if an xGMI all-reduce timed out (one host sync; call at log points)."""
+        if self._xgmi is not None:
+            self._xgmi.check()

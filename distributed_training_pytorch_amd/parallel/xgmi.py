@@ -30,20 +30,26 @@ def slot_granules(P: int) -> int:
     return (P + 1 + 7) & ~7
 
 
-class XgmiExchange:
-    def __init__(self, n_models: int, P: int, device: torch.device, group=None):
+class PeerBuffers:
+    """One zeroed, uncached device buffer per rank, IPC-mapped into every rank.
+
+    ``ptrs[r]`` is rank r's buffer as seen from this process; ``peer_table`` is
+    the same list as a device int64 tensor (what the kernels index).  The handle
+    exchange (``all_gather_object``) happens after every rank zeroed its buffer,
+    so it doubles as the barrier that orders initialisation before first use.
+    """
+
+    def __init__(self, nbytes: int, device: torch.device, group=None):
         self.lib = nat.require(device)
         self.device = device
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.n_models = n_models
-        self.P = P
-        self.bytes = 2 * n_models * self.world * slot_granules(P) * 8
+        self.bytes = nbytes
         self._own = ctypes.c_void_p()
         self._opened: list[int] = []
         torch.cuda.set_device(device)
-        nat.check(self.lib.dtp_malloc_uncached(self.bytes, ctypes.byref(self._own)), "dtp_malloc_uncached")
+        nat.check(self.lib.dtp_malloc_uncached(nbytes, ctypes.byref(self._own)), "dtp_malloc_uncached")
         ptrs = [0] * self.world
         ptrs[self.rank] = self._own.value
         if self.world > 1:
@@ -69,15 +75,8 @@ class XgmiExchange:
                 nat.check(self.lib.dtp_ipc_open_handle(hb, ctypes.byref(p)), "dtp_ipc_open_handle")
                 self._opened.append(p.value)
                 ptrs[r] = p.value
-        self.peer_table = torch.tensor(ptrs, dtype=torch.int64, device=device)
-        self.epoch = torch.zeros(n_models, dtype=torch.int32, device=device)
-        self.status = torch.zeros(16, dtype=torch.int32, device=device)
         self.ptrs = ptrs
-
-    def check_status(self):
-        s = self.status[:2].tolist()
-        if s[0]:
-            raise RuntimeError(f"xGMI exchange timed out on rank {self.rank} at epoch {s[1]} (peer not responding)")
+        self.peer_table = torch.tensor(ptrs, dtype=torch.int64, device=device)
 
     def close(self):
         for p in self._opened:
@@ -92,3 +91,77 @@ class XgmiExchange:
             self.close()
         except Exception:
             pass
+
+
+class XgmiExchange:
+    """Receive buffers of the fused train kernel's in-kernel exchange (MODE_XGMI_*)."""
+
+    def __init__(self, n_models: int, P: int, device: torch.device, group=None):
+        self.device = device
+        self.n_models = n_models
+        self.P = P
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.bufs = PeerBuffers(2 * n_models * world * slot_granules(P) * 8, device, group)
+        self.lib = self.bufs.lib
+        self.world, self.rank = self.bufs.world, self.bufs.rank
+        self.peer_table = self.bufs.peer_table
+        self.ptrs = self.bufs.ptrs
+        self.epoch = torch.zeros(n_models, dtype=torch.int32, device=device)
+        self.status = torch.zeros(16, dtype=torch.int32, device=device)
+
+    def check_status(self):
+        s = self.status[:2].tolist()
+        if s[0]:
+            raise RuntimeError(f"xGMI exchange timed out on rank {self.rank} at epoch {s[1]} (peer not responding)")
+
+    def close(self):
+        self.bufs.close()
+
+
+class XgmiAllReduce:
+    """Stand-alone one-shot all-reduce of small fp32 buffers over xGMI
+    (``csrc/xgmi_allreduce.hip``): FlatDDP's path for buckets up to ``cap``
+    floats on a single node (W <= 8).
+
+    ``all_reduce_(t, scale)`` is asynchronous on the current stream; the epoch
+    advances on the host per call (calls are stream-ordered on every rank).
+    ``check()`` reads the sticky timeout word (one host sync) -- call it at
+    logging/checkpoint boundaries, not per step.
+    """
+
+    MAX_CAP = 1 << 16  # 64 Ki floats: <= 64 blocks, always co-resident with other work
+
+    def __init__(self, cap: int, device: torch.device, group=None, timeout_us: int = 2_000_000):
+        if cap > self.MAX_CAP:
+            raise ValueError(f"xGMI all-reduce capacity {cap} > {self.MAX_CAP} floats; use RCCL for large buckets")
+        self.cap = int(cap)
+        self.device = device
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if self.world > 8:
+            raise ValueError("the xGMI all-reduce serves one node (<= 8 ranks)")
+        self.bufs = PeerBuffers(2 * self.world * self.cap * 8, device, group)
+        self.lib = self.bufs.lib
+        self.rank = self.bufs.rank
+        self.status = torch.zeros(16, dtype=torch.int32, device=device)
+        self.timeout_us = int(timeout_us)
+        self.epoch = 0
+
+    def all_reduce_(self, t: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
+            raise ValueError("xGMI all-reduce takes a contiguous fp32 tensor on this rank's GPU")
+        n = t.numel()
+        if n > self.cap:
+            raise ValueError(f"{n} floats exceed the xGMI all-reduce capacity {self.cap}")
+        self.epoch += 1
+        nat.check(self.lib.dtp_xgmi_allreduce(nat.ptr(t), n, self.cap, nat.ptr(self.bufs.peer_table), self.world,
+                                              self.rank, self.epoch & 0xFFFFFFFF, float(scale), nat.ptr(self.status),
+                                              self.timeout_us, nat.stream_ptr()), "dtp_xgmi_allreduce")
+        return t
+
+    def check(self):
+        s = self.status[:2].tolist()
+        if s[0]:
+            raise RuntimeError(f"xGMI all-reduce timed out on rank {self.rank} at epoch {s[1]}")
+
+    def close(self):
+        self.bufs.close()

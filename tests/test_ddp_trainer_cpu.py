@@ -77,3 +77,22 @@ def test_lightning_style_trainer_two_ranks(tmp_path):
     assert len(ck) == 1 and "step=12" in ck[0].name
     sd = torch.load(ck[0], weights_only=True)
     assert "model_X.layers.0.weight" in sd["state_dict"]
+
+
+def _flatddp_bucket_views(rank, world):
+    """Every bucket must reduce exactly its own slice of the flat grad (regression:
+    a 2-D flat buffer sliced by rows reduced the whole buffer in one bucket)."""
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(0)
+    bank = ModelBank(2)
+    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad, first_bucket_mb=0.0005,
+                  bucket_cap_mb=0.001)
+    sizes = [ddp._grad1d[lo:hi].numel() for lo, hi in ddp._spans]
+    return sizes, sum(hi - lo for lo, hi in ddp._spans)
+
+
+def test_flatddp_bucket_views_cover_the_buffer():
+    res = run_ranks(_flatddp_bucket_views, 2)
+    sizes, total = res[0]
+    assert len(sizes) > 2 and all(s > 0 for s in sizes) and sum(sizes) == total == 742

@@ -53,3 +53,64 @@ def test_rccl_step_path_single_rank():
     assert used == "rccl"
     torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=2e-5)
     torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
+
+
+def _ar_rank(rank, world, n, calls):
+    from distributed_training_pytorch_amd.parallel.xgmi import XgmiAllReduce
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ar = XgmiAllReduce(1 << 14, dev)
+    outs = []
+    for c in range(calls):
+        g = torch.Generator().manual_seed(100 * c + rank)
+        t = torch.randn(n, generator=g).to(dev)
+        if rank == 1 and c % 2 == 0:
+            torch.cuda._sleep(2_000_000)  # uneven arrival: rank 1 late on every other call
+        ar.all_reduce_(t, scale=0.5)
+        outs.append(t.cpu())
+    torch.cuda.synchronize()
+    ar.check()
+    ar.close()
+    return outs
+
+
+def test_xgmi_allreduce_standalone_uneven():
+    n, calls = 5000, 6
+    res = run_ranks(_ar_rank, 2, (n, calls), timeout=300)
+    for c in range(calls):
+        ref = sum(torch.randn(n, generator=torch.Generator().manual_seed(100 * c + r)) for r in range(2)) * 0.5
+        torch.testing.assert_close(res[0][c], ref, rtol=1e-6, atol=1e-6)
+        assert torch.equal(res[0][c], res[1][c]), "ranks disagree"
+
+
+def _ddp_rank(rank, world, comm):
+    from distributed_training_pytorch_amd.models.bank import ModelBank
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    bank = ModelBank(2).to(dev)
+    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad, first_bucket_mb=0.0005, comm=comm)
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(64, 2, generator=g).to(dev)
+    y = torch.randn(64, 1, generator=g).to(dev)
+    grads = []
+    for _ in range(3):
+        bank.zero_grad()
+        ox, oy = ddp(x)
+        (torch.nn.functional.mse_loss(ox, y) + torch.nn.functional.mse_loss(oy, y)).backward()
+        grads.append(bank.flat_grad.cpu().clone())
+    ddp.check_comm()
+    return grads, ddp.comm, len(ddp._buckets)
+
+
+def test_flat_ddp_xgmi_matches_host_path():
+    a = run_ranks(_ddp_rank, 2, ("xgmi",), timeout=300)
+    b = run_ranks(_ddp_rank, 2, ("rccl",), timeout=300)
+    assert a[0][1] == "xgmi" and b[0][1] == "rccl" and a[0][2] > 1
+    for r in range(2):
+        for ga, gb in zip(a[r][0], b[r][0]):
+            torch.testing.assert_close(ga, gb, rtol=1e-6, atol=1e-7)
+    assert all(torch.equal(x, y) for x, y in zip(a[0][0], a[1][0]))
