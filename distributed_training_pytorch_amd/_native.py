@@ -143,6 +143,8 @@ class GemmArgs(ctypes.Structure):
         ("slope", c_float),
         ("vec_a", c_int),
         ("vec_b", c_int),
+        ("force_big", c_int),
+        ("pad_", c_int),
     ]
 
 

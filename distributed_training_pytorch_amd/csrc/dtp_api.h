@@ -111,6 +111,8 @@ struct DtpGemmArgs {
   int splitk;      // >1: K split over blocks, f32 atomics into C
   float alpha, slope;
   int vec_a, vec_b;  // set by dtp_gemm (16-byte loads allowed)
+  int force_big;     // tests: take the 256x256 bf16 kernel for any layout it supports
+  int pad_;
 };
 
 int dtp_gemm(const DtpGemmArgs* a, void* stream);

@@ -62,12 +62,15 @@ DTP_DEV float load_elem(const char* p) {
 
 // 16 bytes of row `r` (memory row), elements [c, c+EPC) of a matrix with `rows` rows,
 // `cols` columns and leading dimension `ld`; out-of-range elements read as 0.
-template <int DT>
+// LEAN: the caller guarantees 16-byte aligned rows and cols % EPC == 0 (no
+// partial chunks): one predicated dwordx4 load, no per-element fallback code.
+template <int DT, bool LEAN = false>
 DTP_DEV uint4 load_chunk(const char* base, long long ld, int r, int c, int rows, int cols, bool vec) {
   using T = Ty<DT>;
   uint4 v = make_uint4(0u, 0u, 0u, 0u);
   if (r >= rows || c >= cols) return v;
   const char* p = base + (static_cast<long long>(r) * ld + c) * T::ES;
+  if constexpr (LEAN) return *reinterpret_cast<const uint4*>(p);
   if (vec && c + T::EPC <= cols) return *reinterpret_cast<const uint4*>(p);
   uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -84,64 +87,118 @@ DTP_DEV uint4 load_chunk(const char* base, long long ld, int r, int c, int rows,
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Staging registers of one operand tile (kBM or kBN rows x BK) for one thread.
+// Staging registers of one operand tile (ROWS rows x BK) for one thread: ROWS/32
+// 16-byte chunks (ROWS x 8 chunks over 256 threads).
+template <int ROWS>
 struct Stage {
-  uint4 v[4];
+  uint4 v[ROWS / 32];
 };
 
-// Operand X(row, k), rows [row0, row0+128), k [k0, k0+BK).
+// Operand X(row, k), rows [row0, row0+ROWS), k [k0, k0+BK).
 //   trans = 0: X(row,k) at base[row*ld + k]    (memory rows = operand rows)
-//   trans = 1: X(row,k) at base[k*ld + row]    (memory rows = k)
-template <int DT, bool TRANS>
-DTP_DEV void stage_load(Stage& s, const char* base, long long ld, int row0, int k0, int R, int K, bool vec, int tid) {
+//   trans = 1: X(row,k) at base[k*ld + row]    (memory rows = k): each thread loads
+//              (4 k-rows x 16 B) blocks and transposes them in registers
+template <int DT, bool TRANS, int ROWS, bool LEAN = false>
+DTP_DEV void stage_load(Stage<ROWS>& s, const char* base, long long ld, int row0, int k0, int R, int K, bool vec,
+                        int tid) {
   using T = Ty<DT>;
   if constexpr (!TRANS) {
     const int c = tid & 7;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < ROWS / 32; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      s.v[i] = load_chunk<DT>(base, ld, row0 + r, k0 + c * T::EPC, R, K, vec);
+      s.v[i] = load_chunk<DT, LEAN>(base, ld, row0 + r, k0 + c * T::EPC, R, K, vec);
     }
   } else {
-    constexpr int RC = kBM / T::EPC;  // row chunks per tile
-    const int mc = tid % RC, kq = tid / RC;
+    constexpr int RC = ROWS / T::EPC;  // row chunks per tile
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s.v[i] = load_chunk<DT>(base, ld, k0 + 4 * kq + i, row0 + mc * T::EPC, K, R, vec);
+    for (int b = 0; b < ROWS / 128; ++b) {
+      const int combo = tid + kThreads * b;
+      const int mc = combo % RC, kq = combo / RC;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        s.v[4 * b + i] = load_chunk<DT, LEAN>(base, ld, k0 + 4 * kq + i, row0 + mc * T::EPC, K, R, vec);
+    }
   }
 }
 
-template <int DT, bool TRANS>
-DTP_DEV void stage_store(const Stage& s, uint4* __restrict__ lds, int tid) {
+template <int DT, bool TRANS, int ROWS>
+DTP_DEV void stage_store(const Stage<ROWS>& s, uint4* __restrict__ lds, int tid) {
   using T = Ty<DT>;
   if constexpr (!TRANS) {
     const int c = tid & 7;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) lds[slot((tid >> 3) + 32 * i, c)] = s.v[i];
-  } else if constexpr (DT == DTP_DT_F32) {
-    // 4 k-rows x 4 rows of floats -> for each row one 16-byte chunk (k = 4kq .. 4kq+3)
-    constexpr int RC = kBM / T::EPC;
-    const int mc = tid % RC, kq = tid / RC;
-    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&s.v[0]);
-    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&s.v[1]);
-    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&s.v[2]);
-    const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&s.v[3]);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) lds[slot(mc * 4 + e, kq)] = make_uint4(w0[e], w1[e], w2[e], w3[e]);
+    for (int i = 0; i < ROWS / 32; ++i) lds[slot((tid >> 3) + 32 * i, c)] = s.v[i];
   } else {
-    // bf16: 4 k-rows x 8 rows -> for each row 8 bytes (k = 4kq .. 4kq+3) = half a chunk
-    constexpr int RC = kBM / T::EPC;
-    const int mc = tid % RC, kq = tid / RC;
-    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&s.v[0]);
-    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&s.v[1]);
-    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&s.v[2]);
-    const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&s.v[3]);
+    constexpr int RC = ROWS / T::EPC;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int sh = (e & 1) * 16, q = e >> 1;
-      const uint32_t lo = ((w0[q] >> sh) & 0xffffu) | (((w1[q] >> sh) & 0xffffu) << 16);
-      const uint32_t hi = ((w2[q] >> sh) & 0xffffu) | (((w3[q] >> sh) & 0xffffu) << 16);
-      uint2* dst = reinterpret_cast<uint2*>(lds + slot(mc * 8 + e, kq >> 1)) + (kq & 1);
-      *dst = make_uint2(lo, hi);
+    for (int b = 0; b < ROWS / 128; ++b) {
+      const int combo = tid + kThreads * b;
+      const int mc = combo % RC, kq = combo / RC;
+      const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&s.v[4 * b + 0]);
+      const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&s.v[4 * b + 1]);
+      const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&s.v[4 * b + 2]);
+      const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&s.v[4 * b + 3]);
+      if constexpr (DT == DTP_DT_F32) {
+        // 4 k-rows x 4 rows of floats -> for each row one 16-byte chunk (k = 4kq .. 4kq+3)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) lds[slot(mc * 4 + e, kq)] = make_uint4(w0[e], w1[e], w2[e], w3[e]);
+      } else {
+        // bf16: 4 k-rows x 8 rows -> for each row 8 bytes (k = 4kq .. 4kq+3) = half a chunk
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int sh = (e & 1) * 16, q = e >> 1;
+          const uint32_t lo = ((w0[q] >> sh) & 0xffffu) | (((w1[q] >> sh) & 0xffffu) << 16);
+          const uint32_t hi = ((w2[q] >> sh) & 0xffffu) | (((w3[q] >> sh) & 0xffffu) << 16);
+          uint2* dst = reinterpret_cast<uint2*>(lds + slot(mc * 8 + e, kq >> 1)) + (kq & 1);
+          *dst = make_uint2(lo, hi);
+        }
+      }
+    }
+  }
+}
+
+// tile decode shared by both kernels: XCD-aware remap (workgroups are dealt
+// round-robin over the 8 XCDs: consecutive tile ids land on one XCD's L2), then
+// 8-row groups of M tiles, split-K innermost
+struct TileId {
+  int m0, n0, ks;
+};
+template <int BMT, int BNT>
+DTP_DEV TileId decode_tile(const DtpGemmArgs& a) {
+  const int tm = (a.M + BMT - 1) / BMT, tn = (a.N + BNT - 1) / BNT;
+  int b = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  TileId id;
+  id.ks = b % a.splitk;
+  const int t = b / a.splitk;
+  const int group = t / (8 * tn), first_m = group * 8;
+  const int gsz = min(tm - first_m, 8);
+  id.m0 = (first_m + (t % (8 * tn)) % gsz) * BMT;
+  id.n0 = ((t % (8 * tn)) / gsz) * BNT;
+  return id;
+}
+
+// fused epilogue of one output element
+template <int DT>
+DTP_DEV void epilogue_store(const DtpGemmArgs& a, char* C, const char* aux, int m, int n, float acc, float bias) {
+  float v = a.alpha * acc + bias;
+  if (aux) v *= leaky_grad_from_out(load_elem<DT>(aux + (static_cast<long long>(m) * a.ldaux + n) * Ty<DT>::ES),
+                                    a.slope);
+  if (a.act) v = leaky(v, a.slope);
+  const long long off = static_cast<long long>(m) * a.ldc + n;
+  if (a.out_dtype == DTP_DT_BF16) {
+    uint16_t* p = reinterpret_cast<uint16_t*>(C) + off;
+    if (a.accumulate) v += bf16_to_f32(*p);
+    *p = f32_to_bf16(v);
+  } else {
+    float* p = reinterpret_cast<float*>(C) + off;
+    if (a.splitk > 1) {
+      atomicAdd(p, v);
+    } else {
+      if (a.accumulate) v += *p;
+      *p = v;
     }
   }
 }
@@ -154,18 +211,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(DtpGemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, lr = lane & 15, lg = lane >> 4;
 
-  // ---- tile decode: XCD-aware remap, then 8-row groups of M tiles ----
-  const int tm = (a.M + kBM - 1) / kBM, tn = (a.N + kBN - 1) / kBN;
-  int b = blockIdx.x;
-  const int nb = gridDim.x;
-  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
-  const int ks = b % a.splitk;
-  const int t = b / a.splitk;
-  const int group = t / (8 * tn), first_m = group * 8;
-  const int gsz = min(tm - first_m, 8);
-  const int pid_m = first_m + (t % (8 * tn)) % gsz;
-  const int pid_n = (t % (8 * tn)) / gsz;
-  const int m0 = pid_m * kBM, n0 = pid_n * kBN;
+  const TileId id = decode_tile<kBM, kBN>(a);
+  const int m0 = id.m0, n0 = id.n0, ks = id.ks;
 
   const int ktiles = (a.K + T::BK - 1) / T::BK;
   const int kper = (ktiles + a.splitk - 1) / a.splitk;
@@ -181,12 +228,12 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(DtpGemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stage sa, sb;
+  Stage<kBM> sa, sb;
   if (kt0 < kt1) {
-    stage_load<DT, TA>(sa, A, a.lda, m0, kt0 * T::BK, a.M, a.K, va, tid);
-    stage_load<DT, TB>(sb, B, a.ldb, n0, kt0 * T::BK, a.N, a.K, vb, tid);
-    stage_store<DT, TA>(sa, lds[0][0], tid);
-    stage_store<DT, TB>(sb, lds[0][1], tid);
+    stage_load<DT, TA, kBM>(sa, A, a.lda, m0, kt0 * T::BK, a.M, a.K, va, tid);
+    stage_load<DT, TB, kBN>(sb, B, a.ldb, n0, kt0 * T::BK, a.N, a.K, vb, tid);
+    stage_store<DT, TA, kBM>(sa, lds[0][0], tid);
+    stage_store<DT, TB, kBN>(sb, lds[0][1], tid);
   }
   __syncthreads();
 
@@ -194,8 +241,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(DtpGemmArgs a) {
     const int buf = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) {
-      stage_load<DT, TA>(sa, A, a.lda, m0, (kt + 1) * T::BK, a.M, a.K, va, tid);
-      stage_load<DT, TB>(sb, B, a.ldb, n0, (kt + 1) * T::BK, a.N, a.K, vb, tid);
+      stage_load<DT, TA, kBM>(sa, A, a.lda, m0, (kt + 1) * T::BK, a.M, a.K, va, tid);
+      stage_load<DT, TB, kBN>(sb, B, a.ldb, n0, (kt + 1) * T::BK, a.N, a.K, vb, tid);
     }
     const uint4* la = lds[buf][0];
     const uint4* lb = lds[buf][1];
@@ -228,8 +275,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(DtpGemmArgs a) {
       }
     }
     if (more) {
-      stage_store<DT, TA>(sa, lds[buf ^ 1][0], tid);
-      stage_store<DT, TB>(sb, lds[buf ^ 1][1], tid);
+      stage_store<DT, TA, kBM>(sa, lds[buf ^ 1][0], tid);
+      stage_store<DT, TB, kBN>(sb, lds[buf ^ 1][1], tid);
     }
     __syncthreads();
   }
@@ -237,39 +284,100 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(DtpGemmArgs a) {
   // ---- epilogue: element (m, n) = acc[i][j][r], m = .. + 4*lg + r, n = .. + lr ----
   char* C = static_cast<char*>(a.C);
   const char* aux = static_cast<const char*>(a.aux);
-  const bool first_split = ks == 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + wn * 64 + 16 * j + lr;
     if (n >= a.N) continue;
-    const float bias = (a.bias && first_split) ? a.bias[n] : 0.f;
+    const float bias = (a.bias && ks == 0) ? a.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * 64 + 16 * i + 4 * lg + r;
-        if (m >= a.M) continue;
-        float v = a.alpha * acc[i][j][r] + bias;
-        if (aux) v *= leaky_grad_from_out(load_elem<DT>(aux + (static_cast<long long>(m) * a.ldaux + n) * Ty<DT>::ES),
-                                          a.slope);
-        if (a.act) v = leaky(v, a.slope);
-        const long long off = static_cast<long long>(m) * a.ldc + n;
-        if (a.out_dtype == DTP_DT_BF16) {
-          uint16_t* p = reinterpret_cast<uint16_t*>(C) + off;
-          if (a.accumulate) v += bf16_to_f32(*p);
-          *p = f32_to_bf16(v);
-        } else {
-          float* p = reinterpret_cast<float*>(C) + off;
-          if (a.splitk > 1) {
-            atomicAdd(p, v);
-          } else {
-            if (a.accumulate) v += *p;
-            *p = v;
-          }
-        }
+        if (m < a.M) epilogue_store<DT>(a, C, aux, m, n, acc[i][j][r], bias);
       }
     }
   }
+}
+
+// 256x256 block tile for large bf16 problems: 4 waves (2x2), each a 128x128 tile
+// of 4x4 v_mfma_f32_32x32x16_bf16 fragments (256 accumulators/lane, one wave per
+// SIMD).  Per K-tile a wave reads 32 ds_read_b128 for 64 MFMAs (2048 MFMA
+// cycles): the LDS port runs at ~25 % instead of the 128x128 kernel's ~100 %
+// (64x64 wave tiles re-read every fragment for only 4 MFMAs).
+template <bool TA, bool TB>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_big_kernel(DtpGemmArgs a) {
+  using T = Ty<DTP_DT_BF16>;
+  constexpr int BM = 256, BN = 256;
+  __shared__ uint4 lds[2][2][BM * kChunks];  // [buffer][A|B][row*8 + chunk]: 128 KiB
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
+  const TileId id = decode_tile<BM, BN>(a);
+  const int m0 = id.m0, n0 = id.n0;
+  const int ktiles = (a.K + T::BK - 1) / T::BK;
+  const char* A = static_cast<const char*>(a.A);
+  const char* B = static_cast<const char*>(a.B);
+  const bool va = a.vec_a != 0, vb = a.vec_b != 0;
+
+  f32x16 acc[16];  // fragment (i, j) = acc[4 * i + j]; every index below is a compile-time constant
+  static_for<0, 16>([&](auto IC) { acc[decltype(IC)::value] = f32x16{}; });
+
+  Stage<BM> sa, sb;
+  stage_load<DTP_DT_BF16, TA, BM, true>(sa, A, a.lda, m0, 0, a.M, a.K, va, tid);
+  stage_load<DTP_DT_BF16, TB, BN, true>(sb, B, a.ldb, n0, 0, a.N, a.K, vb, tid);
+  stage_store<DTP_DT_BF16, TA, BM>(sa, lds[0][0], tid);
+  stage_store<DTP_DT_BF16, TB, BN>(sb, lds[0][1], tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < ktiles;
+    if (more) {
+      stage_load<DTP_DT_BF16, TA, BM, true>(sa, A, a.lda, m0, (kt + 1) * T::BK, a.M, a.K, va, tid);
+      stage_load<DTP_DT_BF16, TB, BN, true>(sb, B, a.ldb, n0, (kt + 1) * T::BK, a.N, a.K, vb, tid);
+    }
+    const uint4* la = lds[buf][0];
+    const uint4* lb = lds[buf][1];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {  // K = 16 per MFMA: chunks 2ks (lanes 0-31), 2ks+1 (lanes 32-63)
+      uint4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = la[slot(wm * 128 + 32 * i + lr, 2 * ks + lh)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = lb[slot(wn * 128 + 32 * j + lr, 2 * ks + lh)];
+      static_for<0, 16>([&](auto IC) {
+        constexpr int q = decltype(IC)::value;
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[q / 4]),
+                                                         __builtin_bit_cast(bf16x8, fb[q % 4]), acc[q], 0, 0, 0);
+      });
+    }
+    if (more) {
+      stage_store<DTP_DT_BF16, TA, BM>(sa, lds[buf ^ 1][0], tid);
+      stage_store<DTP_DT_BF16, TB, BN>(sb, lds[buf ^ 1][1], tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[4i+j][r] is (row = (r&3) + 8*(r>>2) + 4*lh, col = lr) of fragment (i, j)
+  char* C = static_cast<char*>(a.C);
+  const char* aux = static_cast<const char*>(a.aux);
+  static_for<0, 4>([&](auto JC) {
+    constexpr int j = decltype(JC)::value;
+    const int n = n0 + wn * 128 + 32 * j + lr;
+    if (n < a.N) {
+      const float bias = a.bias ? a.bias[n] : 0.f;
+      static_for<0, 4>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        static_for<0, 16>([&](auto RC) {
+          constexpr int r = decltype(RC)::value;
+          const int m = m0 + wm * 128 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m < a.M) epilogue_store<DTP_DT_BF16>(a, C, aux, m, n, acc[4 * i + j][r], bias);
+        });
+      });
+    }
+  });
 }
 
 // out[n] (+)= sum_m X[m*ld + n]: bias gradients.  64 columns x 4 row groups per block,
@@ -323,6 +431,26 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   if (a.splitk > 1 && !a.accumulate) {  // atomics accumulate into C: clear it first
     hipError_t e = hipMemset2DAsync(a.C, sizeof(float) * static_cast<size_t>(a.ldc), 0, sizeof(float) * a.N, a.M, s);
     if (e != hipSuccess) return set_err(2, "dtp_gemm: clearing the split-K output failed");
+  }
+  // big bf16 problems (>= 256 tiles of 256x256, no split-K): the 256x256 kernel
+  const long long big_tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  // lean loads need every row 16-byte aligned and whole 8-element chunks
+  const bool lean = a.vec_a && a.vec_b && (a.trans_a ? a.M : a.K) % 8 == 0 && (a.trans_b ? a.N : a.K) % 8 == 0;
+  // measured (scripts/bench_gemm.py): it beats the 128x128 kernel only with both
+  // operands K-contiguous and >= 2 waves of 256 CUs (8192^2: 790 vs 720 TF/s); its
+  // one-wave-per-SIMD register-transpose staging loses on transposed operands
+  const bool big_ok = a.dtype == DTP_DT_BF16 && a.splitk == 1 && big_tiles >= 512 && a.K >= 256 && lean &&
+                      (a.force_big || (!a.trans_a && !a.trans_b));
+  if (big_ok) {
+    const dim3 gb((unsigned)big_tiles), bb(gemm::kThreads);
+    const int kb = (a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0);
+    switch (kb) {
+      case 0: hipLaunchKernelGGL((gemm::gemm_big_kernel<false, false>), gb, bb, 0, s, a); break;
+      case 1: hipLaunchKernelGGL((gemm::gemm_big_kernel<false, true>), gb, bb, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((gemm::gemm_big_kernel<true, false>), gb, bb, 0, s, a); break;
+      default: hipLaunchKernelGGL((gemm::gemm_big_kernel<true, true>), gb, bb, 0, s, a); break;
+    }
+    return check_launch("dtp_gemm(256x256)");
   }
   const dim3 grid(tm * tn * a.splitk), block(gemm::kThreads);
   const int key = (a.dtype == DTP_DT_BF16 ? 4 : 0) | (a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0);

@@ -59,7 +59,7 @@ def _auto_splitk(M: int, N: int, K: int, dtype: torch.dtype) -> int:
 def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
          out: torch.Tensor | None = None, bias: torch.Tensor | None = None, aux: torch.Tensor | None = None,
          act: bool = False, slope: float = 0.01, accumulate: bool = False, alpha: float = 1.0,
-         splitk: int | None = None, out_dtype: torch.dtype | None = None) -> torch.Tensor:
+         splitk: int | None = None, out_dtype: torch.dtype | None = None, force_big: bool = False) -> torch.Tensor:
     """C[M,N] (+)= epilogue(alpha * A(m,k) B(n,k)).
 
     ``a`` is [M,K] (or [K,M] with ``trans_a``); ``b`` is [N,K] (or [K,N] with ``trans_b``).
@@ -102,6 +102,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     args.trans_a, args.trans_b = int(trans_a), int(trans_b)
     args.act, args.accumulate, args.splitk = int(act), int(accumulate), int(splitk)
     args.alpha, args.slope = float(alpha), float(slope)
+    args.force_big = int(force_big)
     nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
     return out
 

@@ -46,6 +46,21 @@ def test_gemm_bf16_layouts(ta, tb, shape):
     torch.testing.assert_close(cb.float(), c, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_gemm_bf16_big_tile_kernel(ta, tb):
+    """>= 256 tiles of 256x256: the 32x32x16 MFMA kernel; ragged M/N edges, fused epilogue."""
+    M, N, K = 8200, 4000, 320  # 33 x 16 = 528 tiles of 256x256
+    a, b = _ops(M, N, K, ta, tb, torch.bfloat16, 7)
+    bias = torch.randn(N, device=DEV)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1, bias=bias, force_big=True)
+    ref = _ref(a, b, ta, tb) + bias
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=2e-3 * K ** 0.5)
+    cb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, splitk=1, act=True, slope=0.1,
+              force_big=True)
+    torch.testing.assert_close(cb.float(), torch.nn.functional.leaky_relu(ref - bias, 0.1), rtol=1e-2, atol=5e-2)
+
+
 def test_gemm_epilogues():
     M, N, K = 300, 200, 96
     a, b = _ops(M, N, K, False, False, torch.float32, 1)
