@@ -40,14 +40,18 @@ struct Scal {
   }
   static constexpr int fbo(int l) { return fwo(l) + S::din(l) * pad2(S::dout(l)); }
   static constexpr int LF = fwo(NL);
-  static constexpr int bwo(int l) {
-    int o = LF;
-    for (int k = 1; k < l; ++k) o += S::dout(k) * pad2(S::din(k));
+  // per-model global workspace (forward blocks only), 64-float (256 B) aligned;
+  // 64-byte scalar-cache lines it spans
+  static constexpr int WS = (LF + 63) & ~63;
+  static constexpr int NLINES = (LF + 15) / 16;
+  // backward blocks live in LDS: W_l [out][pad4(in)], read as broadcast ds_read_b128
+  static constexpr int pad4(int x) { return (x + 3) & ~3; }
+  static constexpr int lbo(int l) {
+    int o = 0;
+    for (int k = 1; k < l; ++k) o += S::dout(k) * pad4(S::din(k));
     return o;
   }
-  // per-model workspace floats, 64-float (256 B) aligned; 64-byte scalar-cache lines used
-  static constexpr int WS = (bwo(NL) + 63) & ~63;
-  static constexpr int NLINES = (bwo(NL) + 15) / 16;
+  static constexpr int LB = lbo(NL) > 0 ? lbo(NL) : 4;
   // MFMA tiles: first + last layer (and the loss row) packed into one tile when they fit
   static constexpr int O0 = S::dout(0);
   static constexpr int IL = S::din(NL - 1);
@@ -61,7 +65,8 @@ struct Scal {
   static_assert(S::OUT + 1 <= 16, "the loss row must fit under the output rows");
 };
 
-// workspace positions of torch-order parameter p (pb = -1: biases, layer-0 weights)
+// positions of torch-order parameter p: pf in the global forward workspace, pb in
+// the LDS backward blocks (-1: biases, layer-0 weights), tpos in the dW tiles
 template <class S>
 DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos) {
   using SC = Scal<S>;
@@ -75,7 +80,7 @@ DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos) {
     if (p >= S::gw(l) && p < S::gb(l)) {
       const int q = p - S::gw(l), j = q / I, i = q - j * I;
       pf = SC::fwo(l) + i * SC::pad2(O) + j;
-      if constexpr (l >= 1) pb = SC::bwo(l) + j * SC::pad2(I) + i;
+      if constexpr (l >= 1) pb = SC::lbo(l) + j * SC::pad4(I) + i;
       tpos = base + (ro + j) * 16 + co + i;
     } else if (p >= S::gb(l) && p < S::gb(l) + O) {
       const int j = p - S::gb(l);
@@ -209,16 +214,50 @@ DTP_DEV void scal_forward(cfloat* wbase, float (&h)[S::NL + 1][16], float slope)
   });
 }
 
-// input gradient of layer l >= 1 for one sample: dz_{l-1} = (W_l^T dz_l) * act'(h_l);
-// `between(g, NG)` runs inside weight group g (the caller's MFMAs ride there)
-template <class S, int l, class Between>
-DTP_DEV void scal_backward_dx(cfloat* wbase, const float (&h)[S::NL + 1][16], float (&dz)[16], float slope,
-                              Between&& between) {
+// input gradient of layer l >= 1 for one sample: dz_{l-1} = (W_l^T dz_l) * act'(h_l).
+// The layer's whole row-major block is pulled out of LDS first (broadcast
+// ds_read_b128, all in flight at once: LDS returns in order, so the FMAs start
+// as soon as the first rows land), then consumed output-major with input pairs
+// as independent v_pk_fma_f32 chains.
+// MFMA interleave: a wave issues in order, and each v_mfma_f32_16x16x4_f32 holds
+// the MFMA pipe for 32 cycles, so the caller's NK MFMA K-steps are spread one or
+// two per weight row -- between two MFMAs the wave issues that row's ~5 FMAs
+// (the sched_group_barrier pipeline pins the MFMA/VALU alternation), and the
+// layer costs ~NK x 32 cycles instead of MFMA time + FMA time.
+template <class S, int l, int NK, class MfmaK>
+DTP_DEV void lds_backward_dx(const float* __restrict__ wl, const float (&h)[S::NL + 1][16], float (&dz)[16],
+                             float slope, MfmaK&& mfma_k) {
   using SC = Scal<S>;
-  constexpr int I = S::din(l), O = S::dout(l), IP = SC::pad2(I), NP = IP / 2;
-  f32x2 g[NP];
-  static_for<0, NP>([&](auto QC) { g[decltype(QC)::value] = f32x2{0.f, 0.f}; });
-  stream_block<O, IP>(wbase, SC::bwo(l), g, [&](auto JC) { return dz[decltype(JC)::value]; }, between);
+  constexpr int I = S::din(l), O = S::dout(l), IP = SC::pad4(I), NQ = IP / 4;
+  float4 w4[O][NQ];
+  static_for<0, O>([&](auto JC) {
+    constexpr int j = decltype(JC)::value;
+    static_for<0, NQ>([&](auto QC) {
+      constexpr int q = decltype(QC)::value;
+      w4[j][q] = *reinterpret_cast<const float4*>(wl + SC::lbo(l) + j * IP + 4 * q);
+    });
+  });
+  f32x2 g[2 * NQ];
+  static_for<0, 2 * NQ>([&](auto QC) { g[decltype(QC)::value] = f32x2{0.f, 0.f}; });
+  static_for<0, O>([&](auto JC) {
+    constexpr int j = decltype(JC)::value;
+    constexpr int k0 = NK * j / O, k1 = NK * (j + 1) / O;
+    static_for<k0, k1>([&](auto KC) { mfma_k(KC); });
+    const f32x2 d = f32x2{dz[j], dz[j]};
+    static_for<0, NQ>([&](auto QC) {
+      constexpr int q = decltype(QC)::value;
+      if constexpr (4 * q < I) g[2 * q] = __builtin_elementwise_fma(f32x2{w4[j][q].x, w4[j][q].y}, d, g[2 * q]);
+      if constexpr (4 * q + 2 < I)
+        g[2 * q + 1] = __builtin_elementwise_fma(f32x2{w4[j][q].z, w4[j][q].w}, d, g[2 * q + 1]);
+    });
+    if constexpr (k1 > k0) {
+      constexpr int nv = (I + 1) / 2;  // this row's v_pk_fma_f32 count
+      static_for<k0, k1>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, nv / (k1 - k0), 0);     // then VALU
+      });
+    }
+  });
   static_for<0, I>([&](auto IC) {
     constexpr int i = decltype(IC)::value;
     const float v = (i & 1) ? g[i / 2].y : g[i / 2].x;
@@ -240,6 +279,17 @@ DTP_DEV TileOps tile_ops(const float* __restrict__ dzb, const float* __restrict_
   }
   return t;
 }
+// one K-step of the tile on two alternating accumulators
+template <int K>
+DTP_DEV void tile_kstep(const TileOps& t, f32x4& acc0, f32x4& acc1) {
+  const float4& a = t.a[K / 4];
+  const float4& b = t.b[K / 4];
+  const float av = (K % 4 == 0) ? a.x : (K % 4 == 1) ? a.y : (K % 4 == 2) ? a.z : a.w;
+  const float bv = (K % 4 == 0) ? b.x : (K % 4 == 1) ? b.y : (K % 4 == 2) ? b.z : b.w;
+  if constexpr (K & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc1, 0, 0, 0);
+  else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
+}
+
 // K-steps [K0, K1) of the tile on two alternating accumulators
 template <int K0, int K1>
 DTP_DEV void tile_ksteps(const TileOps& t, f32x4& acc0, f32x4& acc1) {

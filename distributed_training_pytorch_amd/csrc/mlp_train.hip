@@ -28,6 +28,7 @@ constexpr int kWaves = kBlock / kWave;
 
 template <class S>
 struct TrainSmem {
+  float wb[Scal<S>::LB];  // backward weight blocks (mlp_scalar.h)
   // per wave: [packed first/last tile | hidden layer] x (dz rows, h rows) -- one hidden
   // buffer suffices: a wave's LDS ops execute in order, so layer l-1's staging
   // writes land after layer l's operand reads were issued; reused for the
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   float* __restrict__ gp = a.params + (size_t)model * P;
   float* __restrict__ ws = a.wsp + (size_t)model * SC::WS;
   for (int e = tid; e < SC::WS; e += kBlock) ws[e] = 0.f;
+  for (int e = tid; e < SC::LB; e += kBlock) sm.wb[e] = 0.f;
   const SamplerCfg smp = a.smp;
   const bool cached = a.cache_data && smp.n * (S::IN + ydim) <= kDataCache;
   if (cached) {
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     if (p < P) {
       pw[k] = gp[p];
       ws[pf[k]] = pw[k];
-      if (pb[k] >= 0) ws[pb[k]] = pw[k];
+      if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
       if (kUpdate) {
         mr[k] = a.opt_m[(size_t)model * P + p];
         if (kAdam) vr[k] = a.opt_v[(size_t)model * P + p];
@@ -218,21 +220,23 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
         if constexpr (l == NL - 1) stage_one(dzb, lane, SC::lossrow(), lpart);
         stage_cols<I>(hb, lane, SC::coloff(l), h[l]);
         stage_one(hb, lane, SC::coloff(l) + I, 1.f);
+        if constexpr (l == 2) if (c0 == 0) DTP_STAMP(16);
         if constexpr (!packed) {
-          // this layer's 16 MFMA K-steps ride inside the dX weight groups (MFMA and
-          // VALU pipes overlap; the wave never idles on either alone)
+          // this layer's 16 MFMA K-steps ride between the dX rows (mlp_scalar.h)
           __builtin_amdgcn_wave_barrier();
           const TileOps to = tile_ops(dzb, hb, lane);
+          if constexpr (l == 2 && PROF) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(to.a[0].x), "v"(to.b[3].w));
+            if (c0 == 0) DTP_STAMP(17);
+          }
           f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
           f32x4& a0 = acc[SC::tile(l)];
-          scal_backward_dx<S, l>(w, h, dz, slope, [&](auto GC, auto NGC) {
-            constexpr int g = decltype(GC)::value, ng = decltype(NGC)::value;
-            tile_ksteps<16 * g / ng, 16 * (g + 1) / ng>(to, a0, a1);
-          });
+          lds_backward_dx<S, l, 16>(sm.wb, h, dz, slope,
+                                    [&](auto KC) { tile_kstep<decltype(KC)::value>(to, a0, a1); });
           a0 += a1;
           __builtin_amdgcn_wave_barrier();
         } else if constexpr (l > 0) {
-          scal_backward_dx<S, l>(w, h, dz, slope, [](auto, auto) {});
+          lds_backward_dx<S, l, 0>(sm.wb, h, dz, slope, [](auto) {});
         }
         if (c0 == 0) DTP_STAMP(24 + l);
       });
@@ -310,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
           if constexpr (kAdam) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
           else sgd_update(pw[k], mr[k], g[k] * a.hp.grad_scale, lr, mom, wd, t == 0);
           ws[pf[k]] = pw[k];
-          if (pb[k] >= 0) ws[pb[k]] = pw[k];
+          if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
         }
       }
     }

@@ -43,8 +43,11 @@ def main():
             d = {NAMES[k]: int(s[k] - s[k - 1]) for k in range(1, 8)}
             d["total_step"] = int(st[0, it, 7] - st[0, it, 0]) if it else 0
             d["wave_bwd_end_rel"] = [int(st[0, it, 8 + w] - st[0, it, 0]) for w in range(4)]
-            fl = [int(st[0, it, 16 + l]) for l in range(8) if int(st[0, it, 16 + l])]
-            d["fwd_layers"] = [int(b - a) for a, b in zip([int(s[1])] + fl[:-1], fl)]
+            # layer-2 backward detail: staged (16), tile operands loaded (17), layer done (24+2)
+            if int(st[0, it, 16]) and int(st[0, it, 17]):
+                d["bwd_l2_detail"] = {"start->staged": int(st[0, it, 16] - st[0, it, 24 + 3]),
+                                      "staged->tile_ops": int(st[0, it, 17] - st[0, it, 16]),
+                                      "tile_ops->done": int(st[0, it, 24 + 2] - st[0, it, 17])}
             bl = [int(st[0, it, 24 + l]) for l in range(8) if int(st[0, it, 24 + l])][::-1]
             d["bwd_layers(top->0)"] = [int(b - a) for a, b in zip([int(s[2])] + bl[:-1], bl)]
             rows.append(d)
