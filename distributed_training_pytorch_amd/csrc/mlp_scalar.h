@@ -52,6 +52,15 @@ struct Scal {
     return o;
   }
   static constexpr int LB = lbo(NL) > 0 ? lbo(NL) : 4;
+  // forward blocks in LDS: W_l^T [in][pad4(out)] then bias [pad4(out)]
+  static constexpr int FT4(int l) { return S::din(l) * pad4(S::dout(l)) + pad4(S::dout(l)); }
+  static constexpr int lfo(int l) {
+    int o = LB;
+    for (int k = 0; k < l; ++k) o += FT4(k);
+    return o;
+  }
+  static constexpr int lfb(int l) { return lfo(l) + S::din(l) * pad4(S::dout(l)); }
+  static constexpr int LW = lfo(NL);  // all weight blocks in LDS
   // MFMA tiles: first + last layer (and the loss row) packed into one tile when they fit
   static constexpr int O0 = S::dout(0);
   static constexpr int IL = S::din(NL - 1);
@@ -68,8 +77,9 @@ struct Scal {
 // positions of torch-order parameter p: pf in the global forward workspace, pb in
 // the LDS backward blocks (-1: biases, layer-0 weights), tpos in the dW tiles
 template <class S>
-DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos) {
+DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos, int& pfl) {
   using SC = Scal<S>;
+  pfl = 0;
   pf = 0;
   pb = -1;
   tpos = 0;
@@ -81,10 +91,12 @@ DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos) {
       const int q = p - S::gw(l), j = q / I, i = q - j * I;
       pf = SC::fwo(l) + i * SC::pad2(O) + j;
       if constexpr (l >= 1) pb = SC::lbo(l) + j * SC::pad4(I) + i;
+      pfl = SC::lfo(l) + i * SC::pad4(O) + j;
       tpos = base + (ro + j) * 16 + co + i;
     } else if (p >= S::gb(l) && p < S::gb(l) + O) {
       const int j = p - S::gb(l);
       pf = SC::fbo(l) + j;
+      pfl = SC::lfb(l) + j;
       tpos = base + (ro + j) * 16 + co + I;  // bias column = constant-1 input
     }
   });
@@ -214,6 +226,66 @@ DTP_DEV void scal_forward(cfloat* wbase, float (&h)[S::NL + 1][16], float slope)
   });
 }
 
+// q-th float4 of a row of N valid floats (row padded to 4): when only 2 floats of the
+// last float4 are valid it is read as a b64 (LDS reads cost by bytes: a 10-float
+// row costs 2.5 b128 instead of 3)
+template <int N, int Q>
+DTP_DEV float4 row_quad(const float* __restrict__ p) {
+  if constexpr (4 * Q + 2 >= N) {
+    const float2 t = *reinterpret_cast<const float2*>(p + 4 * Q);
+    return make_float4(t.x, t.y, 0.f, 0.f);
+  } else {
+    return *reinterpret_cast<const float4*>(p + 4 * Q);
+  }
+}
+
+// forward of one sample from the LDS forward blocks: each layer's whole W^T block
+// (+ bias) is pulled out with broadcast ds_read_b128 (all in flight; LDS returns in
+// order, so the FMAs start as the first rows land), then consumed input-major:
+// every output pair is an independent v_pk_fma_f32 chain.
+template <class S>
+DTP_DEV void lds_forward(const float* __restrict__ wl, float (&h)[S::NL + 1][16], float slope) {
+  using SC = Scal<S>;
+  static_for<0, S::NL>([&](auto LC) {
+    constexpr int l = decltype(LC)::value;
+    constexpr int I = S::din(l), O = S::dout(l), OP = SC::pad4(O), NQ = OP / 4;
+    float4 bq[NQ];
+    float4 w4[I][NQ];
+    static_for<0, NQ>([&](auto QC) {
+      constexpr int q = decltype(QC)::value;
+      bq[q] = row_quad<O, q>(wl + SC::lfb(l));
+    });
+    static_for<0, I>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      static_for<0, NQ>([&](auto QC) {
+        constexpr int q = decltype(QC)::value;
+        w4[i][q] = row_quad<O, q>(wl + SC::lfo(l) + i * OP);
+      });
+    });
+    f32x2 z[2 * NQ];
+    static_for<0, NQ>([&](auto QC) {
+      constexpr int q = decltype(QC)::value;
+      z[2 * q] = f32x2{bq[q].x, bq[q].y};
+      z[2 * q + 1] = f32x2{bq[q].z, bq[q].w};
+    });
+    static_for<0, I>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      const f32x2 hi = f32x2{h[l][i], h[l][i]};
+      static_for<0, NQ>([&](auto QC) {
+        constexpr int q = decltype(QC)::value;
+        if constexpr (4 * q < O) z[2 * q] = __builtin_elementwise_fma(f32x2{w4[i][q].x, w4[i][q].y}, hi, z[2 * q]);
+        if constexpr (4 * q + 2 < O)
+          z[2 * q + 1] = __builtin_elementwise_fma(f32x2{w4[i][q].z, w4[i][q].w}, hi, z[2 * q + 1]);
+      });
+    });
+    static_for<0, O>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      const float v = (j & 1) ? z[j / 2].y : z[j / 2].x;
+      h[l + 1][j] = S::act(l) ? leaky(v, slope) : v;
+    });
+  });
+}
+
 // input gradient of layer l >= 1 for one sample: dz_{l-1} = (W_l^T dz_l) * act'(h_l).
 // The layer's whole row-major block is pulled out of LDS first (broadcast
 // ds_read_b128, all in flight at once: LDS returns in order, so the FMAs start
@@ -234,7 +306,7 @@ DTP_DEV void lds_backward_dx(const float* __restrict__ wl, const float (&h)[S::N
     constexpr int j = decltype(JC)::value;
     static_for<0, NQ>([&](auto QC) {
       constexpr int q = decltype(QC)::value;
-      w4[j][q] = *reinterpret_cast<const float4*>(wl + SC::lbo(l) + j * IP + 4 * q);
+      w4[j][q] = row_quad<I, q>(wl + SC::lbo(l) + j * IP);
     });
   });
   f32x2 g[2 * NQ];

@@ -23,12 +23,15 @@ namespace dtp {
 // floats of dataset staged in LDS: the whole weak-scaling dataset of an 8-GPU
 // node (n = 512 x 8 samples x (2 inputs + 1 target)) stays on-chip
 constexpr int kDataCache = 12288;
+#ifndef DTP_SCALAR_FWD
+#define DTP_SCALAR_FWD 0
+#endif
 constexpr int kPermCap = 2048;    // per-rank epoch permutation kept in LDS
 constexpr int kWaves = kBlock / kWave;
 
 template <class S>
 struct TrainSmem {
-  float wb[Scal<S>::LB];  // backward weight blocks (mlp_scalar.h)
+  float wb[Scal<S>::LW];  // backward + forward weight blocks (mlp_scalar.h)
   // per wave: [packed first/last tile | hidden layer] x (dz rows, h rows) -- one hidden
   // buffer suffices: a wave's LDS ops execute in order, so layer l-1's staging
   // writes land after layer l's operand reads were issued; reused for the
@@ -67,6 +70,8 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
   constexpr bool kUpdate = MODE != DTP_MODE_GRAD;
+  // forward weights: SGPR stream from the global workspace (mlp_scalar.h) or LDS blocks
+  constexpr bool kScalarFwd = DTP_SCALAR_FWD;
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
@@ -78,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   float* __restrict__ gp = a.params + (size_t)model * P;
   float* __restrict__ ws = a.wsp + (size_t)model * SC::WS;
   for (int e = tid; e < SC::WS; e += kBlock) ws[e] = 0.f;
-  for (int e = tid; e < SC::LB; e += kBlock) sm.wb[e] = 0.f;
+  for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   const SamplerCfg smp = a.smp;
   const bool cached = a.cache_data && smp.n * (S::IN + ydim) <= kDataCache;
   if (cached) {
@@ -90,18 +95,19 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   const int yoff = smp.n * S::IN;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int pf[NPT], pb[NPT], tp[NPT];
+  int pf[NPT], pb[NPT], tp[NPT], pfl[NPT];
   float pw[NPT], mr[NPT], vr[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int p = tid + k * kBlock;
-    scal_pos<S>(p < P ? p : 0, pf[k], pb[k], tp[k]);
+    scal_pos<S>(p < P ? p : 0, pf[k], pb[k], tp[k], pfl[k]);
     pw[k] = 0.f;
     mr[k] = 0.f;
     vr[k] = 0.f;
     if (p < P) {
       pw[k] = gp[p];
-      ws[pf[k]] = pw[k];
+      if (kScalarFwd) ws[pf[k]] = pw[k];
+      sm.wb[pfl[k]] = pw[k];
       if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
       if (kUpdate) {
         mr[k] = a.opt_m[(size_t)model * P + p];
@@ -171,9 +177,14 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
           h[0][i] = valid ? Xg[(size_t)di * S::IN + i] : 0.f;
         });
       }
-      if (c0 == 0) w = fresh_weights<SC::NLINES>(ws);
-      if (c0 == 0) DTP_STAMP(1);
-      scal_forward<S>(w, h, slope);
+      if constexpr (kScalarFwd) {
+        if (c0 == 0) w = fresh_weights<SC::NLINES>(ws);
+        if (c0 == 0) DTP_STAMP(1);
+        scal_forward<S>(w, h, slope);
+      } else {
+        if (c0 == 0) DTP_STAMP(1);
+        lds_forward<S>(sm.wb, h, slope);
+      }
 
       // ---------------- loss (MSE / CE) -> dz of the last layer
       constexpr int L = NL - 1;
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     __syncthreads();
     // no wave loads this step's weights any more: drop them from the scalar cache
     // before the optimizer writes the new ones (mlp_scalar.h protocol)
-    if (wave == 0) __builtin_amdgcn_s_dcache_inv();
+    if (kScalarFwd && wave == 0) __builtin_amdgcn_s_dcache_inv();
     DTP_STAMP(4);
 
     const float* red = &sm.stage[0][0][0];
@@ -313,7 +324,8 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
         if (p < P) {
           if constexpr (kAdam) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
           else sgd_update(pw[k], mr[k], g[k] * a.hp.grad_scale, lr, mom, wd, t == 0);
-          ws[pf[k]] = pw[k];
+          if (kScalarFwd) ws[pf[k]] = pw[k];
+          sm.wb[pfl[k]] = pw[k];
           if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
         }
       }
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       if (use_perm && it + 1 < a.n_steps) fill_perm(epoch);  // ordered by the barrier below
     }
     if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight stores reached L2 before the barrier
+    if (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight stores reached L2 before the barrier
     __syncthreads();  // updated weights visible; reduction tiles consumed
     DTP_STAMP(7);
   }
