@@ -23,6 +23,9 @@ namespace dtp {
 // floats of dataset staged in LDS: the whole weak-scaling dataset of an 8-GPU
 // node (n = 512 x 8 samples x (2 inputs + 1 target)) stays on-chip
 constexpr int kDataCache = 12288;
+// Adam bias-correction scalars of the next kAdamTab steps, formed cooperatively in
+// f64 (torch's host math) once per kAdamTab steps instead of per step
+constexpr int kAdamTab = 1024;
 #ifndef DTP_SCALAR_FWD
 #define DTP_SCALAR_FWD 0
 #endif
@@ -32,6 +35,7 @@ constexpr int kWaves = kBlock / kWave;
 template <class S>
 struct TrainSmem {
   float wb[Scal<S>::LW];  // backward + forward weight blocks (mlp_scalar.h)
+  float2 adam_tab[kAdamTab];  // per-step Adam scalars {lr / (1 - b1^t), sqrt(1 - b2^t)}
   // per wave: [packed first/last tile | hidden layer] x (dz rows, h rows) -- one hidden
   // buffer suffices: a wave's LDS ops execute in order, so layer l-1's staging
   // writes land after layer l's operand reads were issued; reused for the
@@ -133,8 +137,15 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   };
   if (use_perm) fill_perm(epoch);
   // Adam bias-correction powers beta^t, carried in double like torch's host math
-  double b1t = kAdam ? pow_int(a.hp.beta1, (uint64_t)t0) : 1.0;
-  double b2t = kAdam ? pow_int(a.hp.beta2, (uint64_t)t0) : 1.0;
+  // table entry e holds the scalars of step number t0 + base + e + 1
+  auto fill_adam = [&](int base) {
+    for (int e = tid; e < kAdamTab; e += kBlock) {
+      const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
+      const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
+      sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
+    }
+  };
+  if (kAdam) fill_adam(0);
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
   float* const stg_pack = &sm.stage[wave][0][0];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -151,8 +162,10 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     const int bsz = bp.size;
     const float inv = ce ? 1.f / (float)bsz : 1.f / (float)(bsz * S::OUT);
     // this step's optimizer scalars, off the critical path (overlaps the forward)
-    AdamScalars as{};
-    if constexpr (kAdam) as = adam_scalars_from_pow(a.hp, b1t * a.hp.beta1, b2t * a.hp.beta2);
+    if (kAdam && it > 0 && it % kAdamTab == 0) {  // ordered by the step's barriers before its use
+      __syncthreads();
+      fill_adam(it);
+    }
 
     f32x4 acc[NT];
 #pragma unroll
@@ -313,9 +326,11 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       }
       if (tid == 0) a.grad_out[(size_t)a.n_models * P + model] = mean_loss;
     } else {
+      AdamScalars as = adam_consts(a.hp);
       if constexpr (kAdam) {
-        b1t *= a.hp.beta1;
-        b2t *= a.hp.beta2;
+        const float2 sc = sm.adam_tab[it % kAdamTab];
+        as.step_size = sc.x;
+        as.bc2_sqrt = sc.y;
       }
       const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
 #pragma unroll

@@ -43,6 +43,19 @@ DTP_DEV AdamScalars adam_scalars_from_pow(const DtpHyper& hp, double b1t, double
   return s;
 }
 
+// the step-independent part of the scalars (step_size / bc2_sqrt filled by the caller)
+DTP_DEV AdamScalars adam_consts(const DtpHyper& hp) {
+  AdamScalars s;
+  s.step_size = 0.f;
+  s.bc2_sqrt = 1.f;
+  s.one_m_b1 = (float)(1.0 - hp.beta1);
+  s.b2 = (float)hp.beta2;
+  s.one_m_b2 = (float)(1.0 - hp.beta2);
+  s.eps = (float)hp.eps;
+  s.wd = (float)hp.weight_decay;
+  return s;
+}
+
 DTP_DEV void adam_update(float& p, float& m, float& v, float g, const AdamScalars& s) {
   if (s.wd != 0.f) g = g + s.wd * p;
   m = m + s.one_m_b1 * (g - m);
