@@ -139,7 +139,8 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   // Adam bias-correction powers beta^t, carried in double like torch's host math
   // table entry e holds the scalars of step number t0 + base + e + 1
   auto fill_adam = [&](int base) {
-    for (int e = tid; e < kAdamTab; e += kBlock) {
+    const int n = min(kAdamTab, a.n_steps - base);  // short launches (eager / graph) fill only what they use
+    for (int e = tid; e < n; e += kBlock) {
       const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
       const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
       sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
