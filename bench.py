@@ -60,12 +60,18 @@ def parse():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:(local_rank %% device_count), gloo process group "
+                         "(exercises the multi-rank path on a 1-GPU box; numbers are not scaling numbers)")
     return ap.parse_args()
 
 
 def main():
     a = parse()
-    rank, world, local_rank = dist_env.init_from_env(single_rank_pg=a.impl == "stock")
+    if a.share_gpu and torch.cuda.device_count() > 0:
+        os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+    rank, world, local_rank = dist_env.init_from_env(backend="gloo" if a.share_gpu else None,
+                                                     single_rank_pg=a.impl == "stock")
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
     dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")

@@ -52,10 +52,15 @@ def barrier():
             dist.barrier()
 
 
+def _scalar_device(device):
+    # gloo reduces host tensors; RCCL device tensors
+    return device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
 def allreduce_max(x: float, device) -> float:
     if not dist.is_initialized():
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=_scalar_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -63,6 +68,6 @@ def allreduce_max(x: float, device) -> float:
 def allreduce_sum(x: float, device) -> float:
     if not dist.is_initialized():
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=_scalar_device(device))
     dist.all_reduce(t)
     return float(t.item())
