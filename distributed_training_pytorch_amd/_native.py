@@ -144,7 +144,7 @@ class GemmArgs(ctypes.Structure):
         ("vec_a", c_int),
         ("vec_b", c_int),
         ("force_big", c_int),
-        ("pad_", c_int),
+        ("fast", c_int),
     ]
 
 

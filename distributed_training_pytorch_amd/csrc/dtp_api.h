@@ -112,7 +112,7 @@ struct DtpGemmArgs {
   float alpha, slope;
   int vec_a, vec_b;  // set by dtp_gemm (16-byte loads allowed)
   int force_big;     // tests: take the 256x256 bf16 kernel for any layout it supports
-  int pad_;
+  int fast;          // LDS-DMA 256x256 bf16 kernel: 0 auto, 1 whenever its preconditions hold, -1 never
 };
 
 int dtp_gemm(const DtpGemmArgs* a, void* stream);

@@ -380,6 +380,172 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   });
 }
 
+// ---------------------------------------------------------------------------
+// Fast bf16 GEMM: 256x256x64 tiles, 8 waves (2 x 4, each 128 x 64 of
+// v_mfma_f32_16x16x32_bf16), operands staged global -> LDS by the gfx950 LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave instruction): no staging registers
+// and no ds_write pass, so each SIMD's two waves hold 128 accumulators plus a
+// k-step of fragments and one wave's MFMAs cover the other's LDS reads.  Every
+// operand layout of an MLP layer runs here:
+//  * K-contiguous operand (x and W of the forward, dz of dx = dz W): LDS image
+//    [256 rows][8 x 16-B chunks]; a fragment is one ds_read_b128;
+//  * M/N-contiguous operand (W of dx = dz W; dz and h of dW = dz^T h): LDS image
+//    [64 k][256 columns] exactly as in memory; a fragment is two
+//    ds_read_b64_tr_b16 (gfx950's transposing LDS read): no register transpose.
+// Bank swizzles ride on the DMA SOURCE address (the DMA writes lane-linear),
+// both with fswz(x) = (x & 3) | ((x >> 1) & 4):
+//  * row image: physical chunk p of row r holds logical chunk p ^ fswz(r); the
+//    four 16-lane groups of a ds_read_b128 ({0-3,12-15,20-27}, ...) then hit 16
+//    distinct 16-B bank slots (conflict-free), and fswz depends on r & 15 only,
+//    so all fragments of a wave share one lane address + immediate offsets;
+//  * k-major image: the 32-B granule g of k-row k sits at g ^ fswz(k); the eight
+//    k-rows one 32-lane half of a transposing read touches land in 8 distinct
+//    32-B windows of the 256-B bank row (conflict-free).
+// Pipeline: tile t+1's DMA is issued before tile t's ds_read/MFMA block; one
+// vmcnt(0) + barrier per K-tile retires it (RAW) and frees tile t's buffer for
+// tile t+2's DMA (WAR).  Preconditions (dtp_gemm checks them): K % 64 == 0,
+// 16-byte aligned rows, a transposed operand's M/N a multiple of 8.  Rows or
+// columns past M / N are clamped on load and never stored.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+constexpr int kFastThreads = 512;
+constexpr int kFastImg = 256 * 64 * 2;  // bytes of one operand image (one K-tile)
+
+DTP_DEV int fswz(int x) { return (x & 3) | ((x >> 1) & 4); }
+
+// Per-lane DMA sources of the 4 instructions that fill one operand image:
+// instruction i of wave w fills image bytes [(8 i + w) KiB, +1 KiB).
+template <bool TRANS>
+DTP_DEV void fast_sources(const char* (&src)[4], const char* base, long long ld, int r0, int R, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (!TRANS) {  // 8 rows x 128 B: row (8i+w)*8 + lane/8, physical chunk lane%8
+      const int row = (8 * i + wave) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ fswz(row);
+      const int rr = min(r0 + row, R - 1);
+      src[i] = base + (static_cast<long long>(rr) * ld + c * 8) * 2;
+    } else {  // 2 k-rows x 512 B: k = (8i+w)*2 + lane/32, physical chunk lane%32
+      const int k = (8 * i + wave) * 2 + (lane >> 5);
+      const int c = (lane & 31) ^ (fswz(k) << 1);
+      const int col = min(r0 + c * 8, R - 8);
+      src[i] = base + (static_cast<long long>(k) * ld + col) * 2;
+    }
+  }
+}
+
+// Byte offsets (inside an image) of this lane's fragment reads.  Row image:
+// off[ks] for k-step ks, fragment f adds 2048 f.  k-major image: off[f] for
+// fragment f at k-step 0; k-step 1 adds 16384, the upper 4 k of a fragment 2048.
+template <bool TRANS, int NF>
+DTP_DEV void fast_offsets(int (&off)[TRANS ? NF : 2], int rb, int lane) {
+  const int lr = lane & 15, lg = lane >> 4;
+  if constexpr (!TRANS) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) off[ks] = ((rb + lr) * 8 + ((4 * ks + lg) ^ fswz(lr))) * 16;
+  } else {
+    // lane 4q+p of group lg supplies k-row 8 lg + q (+ 32 ks, + 4), columns 4p..4p+3
+    const int q = lr >> 2, p = lr & 3, sw = q | ((lg & 1) << 2);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) off[f] = (8 * lg + q) * 512 + (((rb + 16 * f) * 2) ^ (sw << 5)) + 8 * p;
+  }
+}
+
+template <bool TRANS>
+DTP_DEV bf16x8 fast_frag(const char* img, const int* off, int f, int ks) {
+  if constexpr (!TRANS) {
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + off[ks] + f * 2048));
+  } else {
+    const char* p = img + off[f] + ks * 16384;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 2048));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 64;
+  __shared__ __align__(16) char lds[2 * 2 * kFastImg];  // [buffer][A | B] images: 128 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3, lr = lane & 15, lg = lane >> 4;
+  const TileId id = decode_tile<BM, BN>(a);
+  const int m0 = id.m0, n0 = id.n0, nk = a.K / BK;
+
+  const char* srcA[4];
+  const char* srcB[4];
+  fast_sources<TA>(srcA, static_cast<const char*>(a.A), a.lda, m0, a.M, wave, lane);
+  fast_sources<TB>(srcB, static_cast<const char*>(a.B), a.ldb, n0, a.N, wave, lane);
+  const long long kbA = TA ? static_cast<long long>(BK) * a.lda * 2 : BK * 2;
+  const long long kbB = TB ? static_cast<long long>(BK) * a.ldb * 2 : BK * 2;
+  auto stage = [&](int buf, int kt) {
+    char* img = lds + buf * 2 * kFastImg;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcA[i] + kt * kbA), (lds_void_t*)(img + (8 * i + wave) * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[i] + kt * kbB),
+                                       (lds_void_t*)(img + kFastImg + (8 * i + wave) * 1024), 16, 0, 0);
+    }
+  };
+  int offA[TA ? 8 : 2], offB[TB ? 4 : 2];
+  fast_offsets<TA, 8>(offA, wr * 128, lane);
+  fast_offsets<TB, 4>(offB, wc * 64, lane);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
+    const char* ia = lds + buf * 2 * kFastImg;
+    const char* ib = ia + kFastImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[8], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = fast_frag<TB>(ib, offB, j, ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = fast_frag<TA>(ia, offA, i, ks);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] = C(row wr*128 + 16 i + 4 lg + r, col wc*64 + 16 j + lr)
+  char* C = static_cast<char*>(a.C);
+  const char* aux = static_cast<const char*>(a.aux);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + 16 * j + lr;
+    if (n >= a.N) continue;
+    const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + 16 * i + 4 * lg + r;
+        if (m < a.M) epilogue_store<DTP_DT_BF16>(a, C, aux, m, n, acc[i][j][r], bias);
+      }
+    }
+  }
+}
+
 // out[n] (+)= sum_m X[m*ld + n]: bias gradients.  64 columns x 4 row groups per block,
 // 1024 rows per block; partial sums of several row blocks meet in f32 atomics.
 template <int DT>
@@ -434,6 +600,21 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   }
   // big bf16 problems (>= 256 tiles of 256x256, no split-K): the 256x256 kernel
   const long long big_tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  // the LDS-DMA 256x256 kernel: whole 64-deep K tiles, 16-byte aligned rows, a
+  // transposed operand in whole 8-element chunks; by default once there are
+  // enough 256x256 tiles to occupy half the chip's CUs
+  const bool fast_shape = a.dtype == DTP_DT_BF16 && a.splitk == 1 && a.K % 64 == 0 && a.vec_a && a.vec_b &&
+                          (!a.trans_a || a.M % 8 == 0) && (!a.trans_b || a.N % 8 == 0) && !a.force_big;
+  if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
+    const dim3 gf((unsigned)big_tiles), bf(gemm::kFastThreads);
+    switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
+      case 0: hipLaunchKernelGGL((gemm::gemm_fast_kernel<false, false>), gf, bf, 0, s, a); break;
+      case 1: hipLaunchKernelGGL((gemm::gemm_fast_kernel<false, true>), gf, bf, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((gemm::gemm_fast_kernel<true, false>), gf, bf, 0, s, a); break;
+      default: hipLaunchKernelGGL((gemm::gemm_fast_kernel<true, true>), gf, bf, 0, s, a); break;
+    }
+    return check_launch("dtp_gemm(LDS-DMA 256x256)");
+  }
   // lean loads need every row 16-byte aligned and whole 8-element chunks
   const bool lean = a.vec_a && a.vec_b && (a.trans_a ? a.M : a.K) % 8 == 0 && (a.trans_b ? a.N : a.K) % 8 == 0;
   // measured (scripts/bench_gemm.py): it beats the 128x128 kernel only with both

@@ -59,11 +59,14 @@ def _auto_splitk(M: int, N: int, K: int, dtype: torch.dtype) -> int:
 def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
          out: torch.Tensor | None = None, bias: torch.Tensor | None = None, aux: torch.Tensor | None = None,
          act: bool = False, slope: float = 0.01, accumulate: bool = False, alpha: float = 1.0,
-         splitk: int | None = None, out_dtype: torch.dtype | None = None, force_big: bool = False) -> torch.Tensor:
+         splitk: int | None = None, out_dtype: torch.dtype | None = None, force_big: bool = False,
+         fast: bool | None = None) -> torch.Tensor:
     """C[M,N] (+)= epilogue(alpha * A(m,k) B(n,k)).
 
     ``a`` is [M,K] (or [K,M] with ``trans_a``); ``b`` is [N,K] (or [K,N] with ``trans_b``).
     Epilogue order: + bias[n], * LeakyReLU'(aux[m,n]), LeakyReLU, (+ old C), cast.
+    ``fast``: None = pick the kernel by shape; True = the LDS-DMA 256x256 bf16 kernel
+    whenever its preconditions hold (K % 64 == 0, aligned rows); False = never.
     """
     M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
     N, Kb = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
@@ -103,6 +106,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     args.act, args.accumulate, args.splitk = int(act), int(accumulate), int(splitk)
     args.alpha, args.slope = float(alpha), float(slope)
     args.force_big = int(force_big)
+    args.fast = 0 if fast is None else (1 if fast else -1)
     nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
     return out
 
