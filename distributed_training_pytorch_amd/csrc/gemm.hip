@@ -466,7 +466,10 @@ DTP_DEV bf16x8 fast_frag(const char* img, const int* off, int f, int ks) {
   }
 }
 
-template <bool TA, bool TB>
+// VAR (schedule experiments, selected by DtpGemmArgs::fast = 2 + VAR): bit 0 = static
+// s_setprio(1) for waves 4-7 instead of per-cluster flips; bit 1 = the next tile's
+// DMA split over the two k-steps (4 pieces ahead of each MFMA cluster)
+template <bool TA, bool TB, int VAR>
 __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64;
   __shared__ __align__(16) char lds[2 * 2 * kFastImg];  // [buffer][A | B] images: 128 KiB
@@ -481,10 +484,10 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
   fast_sources<TB>(srcB, static_cast<const char*>(a.B), a.ldb, n0, a.N, wave, lane);
   const long long kbA = TA ? static_cast<long long>(BK) * a.lda * 2 : BK * 2;
   const long long kbB = TB ? static_cast<long long>(BK) * a.ldb * 2 : BK * 2;
-  auto stage = [&](int buf, int kt) {
+  auto stage = [&](int buf, int kt, int i0, int i1) {
     char* img = lds + buf * 2 * kFastImg;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = i0; i < i1; ++i) {
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcA[i] + kt * kbA), (lds_void_t*)(img + (8 * i + wave) * 1024),
                                        16, 0, 0);
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[i] + kt * kbB),
@@ -501,12 +504,20 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, 0);
+  constexpr bool kStaticPrio = VAR & 1, kSplitDma = VAR & 2;
+  if constexpr (kStaticPrio) {
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+  stage(0, 0, 0, 4);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      if constexpr (kSplitDma) stage(buf ^ 1, kt + 1, 0, 2);
+      else stage(buf ^ 1, kt + 1, 0, 4);
+    }
     const char* ia = lds + buf * 2 * kFastImg;
     const char* ib = ia + kFastImg;
 #pragma unroll
@@ -516,12 +527,15 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
       for (int j = 0; j < 4; ++j) fb[j] = fast_frag<TB>(ib, offB, j, ks);
 #pragma unroll
       for (int i = 0; i < 8; ++i) fa[i] = fast_frag<TA>(ia, offA, i, ks);
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (kSplitDma) {
+        if (ks == 1 && more) stage(buf ^ 1, kt + 1, 2, 4);
+      }
+      if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -544,6 +558,21 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
       }
     }
   }
+}
+
+constexpr int kFastDefaultVar = 1;  // static waves-4-7 priority: +2-6 % over var 0 (profiles/gemm_r1_fast/variants.jsonl)
+
+template <int VAR>
+int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
+  const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const dim3 gf((unsigned)tiles), bf(kFastThreads);
+  switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
+    case 0: hipLaunchKernelGGL((gemm_fast_kernel<false, false, VAR>), gf, bf, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((gemm_fast_kernel<false, true, VAR>), gf, bf, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_fast_kernel<true, false, VAR>), gf, bf, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_fast_kernel<true, true, VAR>), gf, bf, 0, s, a); break;
+  }
+  return check_launch("dtp_gemm(LDS-DMA 256x256)");
 }
 
 // out[n] (+)= sum_m X[m*ld + n]: bias gradients.  64 columns x 4 row groups per block,
@@ -606,14 +635,13 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   const bool fast_shape = a.dtype == DTP_DT_BF16 && a.splitk == 1 && a.K % 64 == 0 && a.vec_a && a.vec_b &&
                           (!a.trans_a || a.M % 8 == 0) && (!a.trans_b || a.N % 8 == 0) && !a.force_big;
   if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
-    const dim3 gf((unsigned)big_tiles), bf(gemm::kFastThreads);
-    switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
-      case 0: hipLaunchKernelGGL((gemm::gemm_fast_kernel<false, false>), gf, bf, 0, s, a); break;
-      case 1: hipLaunchKernelGGL((gemm::gemm_fast_kernel<false, true>), gf, bf, 0, s, a); break;
-      case 2: hipLaunchKernelGGL((gemm::gemm_fast_kernel<true, false>), gf, bf, 0, s, a); break;
-      default: hipLaunchKernelGGL((gemm::gemm_fast_kernel<true, true>), gf, bf, 0, s, a); break;
+    const int var = a.fast >= 2 ? (a.fast - 2) & 3 : gemm::kFastDefaultVar;
+    switch (var) {
+      case 0: return gemm::launch_fast<0>(a, s);
+      case 1: return gemm::launch_fast<1>(a, s);
+      case 2: return gemm::launch_fast<2>(a, s);
+      default: return gemm::launch_fast<3>(a, s);
     }
-    return check_launch("dtp_gemm(LDS-DMA 256x256)");
   }
   // lean loads need every row 16-byte aligned and whole 8-element chunks
   const bool lean = a.vec_a && a.vec_b && (a.trans_a ? a.M : a.K) % 8 == 0 && (a.trans_b ? a.N : a.K) % 8 == 0;

@@ -60,7 +60,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
          out: torch.Tensor | None = None, bias: torch.Tensor | None = None, aux: torch.Tensor | None = None,
          act: bool = False, slope: float = 0.01, accumulate: bool = False, alpha: float = 1.0,
          splitk: int | None = None, out_dtype: torch.dtype | None = None, force_big: bool = False,
-         fast: bool | None = None) -> torch.Tensor:
+         fast: bool | int | None = None) -> torch.Tensor:
     """C[M,N] (+)= epilogue(alpha * A(m,k) B(n,k)).
 
     ``a`` is [M,K] (or [K,M] with ``trans_a``); ``b`` is [N,K] (or [K,N] with ``trans_b``).
@@ -106,7 +106,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     args.act, args.accumulate, args.splitk = int(act), int(accumulate), int(splitk)
     args.alpha, args.slope = float(alpha), float(slope)
     args.force_big = int(force_big)
-    args.fast = 0 if fast is None else (1 if fast else -1)
+    # int >= 2: force the fast kernel with schedule variant fast - 2 (experiments / benches)
+    args.fast = 0 if fast is None else (int(fast) if fast is not True and fast is not False else (1 if fast else -1))
     nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
     return out
 
