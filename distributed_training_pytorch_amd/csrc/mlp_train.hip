@@ -29,7 +29,6 @@ constexpr int kAdamTab = 1024;
 #ifndef DTP_SCALAR_FWD
 #define DTP_SCALAR_FWD 0
 #endif
-constexpr int kPermCap = 2048;    // per-rank epoch permutation kept in LDS
 constexpr int kWaves = kBlock / kWave;
 
 template <class S>
@@ -42,7 +41,15 @@ struct TrainSmem {
   // cross-wave dW tile reduction
   float stage[kWaves][2][2 * kStgArr];
   float data[kDataCache];
-  int perm[kPermCap];
+  float sink[4];  // target of the optimizer's predicated-off stores (slots past P)
+};
+
+// One lane's sample of a step: input, target (class index for CE) and validity.
+template <class S>
+struct SampleRegs {
+  float x[S::IN];
+  float y[S::OUT];
+  bool valid;
 };
 
 // In-kernel phase stamps (diagnostic instantiation only, PROF = true): lane 0 of
@@ -127,15 +134,36 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
   uint32_t keys[4];
   epoch_keys(smp, epoch, keys);
-  // the shuffled epoch order is computed once per epoch into LDS (cooperatively)
-  const bool use_perm = smp.mode == SAMPLER_DIST_SHUFFLE && smp.num_samples <= kPermCap;
-  auto fill_perm = [&](int ep) {
-    uint32_t kk[4];
-    epoch_keys(smp, ep, kk);
-    const BatchPos b0{ep, 0, 0};
-    for (int pos = tid; pos < smp.num_samples; pos += kBlock) sm.perm[pos] = sample_index(smp, b0, kk, pos);
+  // sample k of step it (batch geometry bp): index (explicit list or the in-kernel
+  // Feistel shuffle, sampler.h) -> input and target from the LDS-resident dataset.
+  // The next step's first chunk is gathered while the current step's optimizer
+  // runs (the sampler depends on nothing the update writes), so a step starts
+  // with its inputs already in registers.
+  auto gather = [&](int it_, const BatchPos& bp_, const uint32_t (&keys_)[4], int k, int bsz_) {
+    SampleRegs<S> r;
+    r.valid = k < bsz_;
+    int di = 0;
+    if (r.valid) di = explicit_idx ? a.idx[(size_t)it_ * smp.batch + k] : sample_index(smp, bp_, keys_, k);
+    static_for<0, S::IN>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      r.x[i] = r.valid ? (cached ? sm.data[di * S::IN + i] : Xg[(size_t)di * S::IN + i]) : 0.f;
+    });
+    static_for<0, S::OUT>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      float y = 0.f;
+      if (r.valid && j < ydim) y = cached ? sm.data[yoff + di * ydim + j] : Yg[(size_t)di * ydim + j];
+      r.y[j] = y;
+    });
+    return r;
   };
-  if (use_perm) fill_perm(epoch);
+  auto batch_at = [&](int ep, int b) {
+    BatchPos bp_;
+    bp_.epoch = ep;
+    bp_.start = b * smp.batch;
+    bp_.size = explicit_idx ? smp.batch : min(smp.batch, smp.num_samples - bp_.start);
+    return bp_;
+  };
+  SampleRegs<S> nxt = gather(0, batch_at(epoch, bi), keys, tid, batch_at(epoch, bi).size);
   // Adam bias-correction powers beta^t, carried in double like torch's host math
   // table entry e holds the scalars of step number t0 + base + e + 1
   auto fill_adam = [&](int base) {
@@ -156,10 +184,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     DTP_STAMP(0);
     cfloat* w = nullptr;
     const int t = t0 + it;
-    BatchPos bp;
-    bp.epoch = epoch;
-    bp.start = bi * smp.batch;
-    bp.size = explicit_idx ? smp.batch : min(smp.batch, smp.num_samples - bp.start);
+    const BatchPos bp = batch_at(epoch, bi);
     const int bsz = bp.size;
     const float inv = ce ? 1.f / (float)bsz : 1.f / (float)(bsz * S::OUT);
     // this step's optimizer scalars, off the critical path (overlaps the forward)
@@ -173,24 +198,10 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int c0 = 0; c0 < bsz; c0 += kBlock) {
-      const int k = c0 + tid;
-      const bool valid = k < bsz;
-      int di = 0;
-      if (valid)
-        di = explicit_idx ? a.idx[(size_t)it * smp.batch + k]
-                          : (use_perm ? sm.perm[bp.start + k] : sample_index(smp, bp, keys, k));
+      const SampleRegs<S> smpl = c0 == 0 ? nxt : gather(it, bp, keys, c0 + tid, bsz);
+      const bool valid = smpl.valid;
       float h[NL + 1][16];
-      if (cached) {
-        static_for<0, S::IN>([&](auto IC) {
-          constexpr int i = decltype(IC)::value;
-          h[0][i] = valid ? sm.data[di * S::IN + i] : 0.f;
-        });
-      } else {
-        static_for<0, S::IN>([&](auto IC) {
-          constexpr int i = decltype(IC)::value;
-          h[0][i] = valid ? Xg[(size_t)di * S::IN + i] : 0.f;
-        });
-      }
+      static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = smpl.x[decltype(IC)::value]; });
       if constexpr (kScalarFwd) {
         if (c0 == 0) w = fresh_weights<SC::NLINES>(ws);
         if (c0 == 0) DTP_STAMP(1);
@@ -207,14 +218,12 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       if (!ce) {
         static_for<0, S::OUT>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
-          float y = 0.f;
-          if (valid) y = cached ? sm.data[yoff + di * S::OUT + j] : Yg[(size_t)di * S::OUT + j];
-          const float d = h[L + 1][j] - y;
+          const float d = h[L + 1][j] - smpl.y[j];
           lpart += valid ? d * d : 0.f;
           dz[j] = valid ? 2.f * d * inv : 0.f;
         });
       } else {
-        const int cls = valid ? (int)(cached ? sm.data[yoff + di] : Yg[di]) : 0;
+        const int cls = valid ? (int)smpl.y[0] : 0;
         float mx = h[L + 1][0];
         static_for<1, S::OUT>([&](auto JC) { mx = fmaxf(mx, h[L + 1][decltype(JC)::value]); });
         float se = 0.f, zc = 0.f;
@@ -274,6 +283,9 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     DTP_STAMP(8 + wave);
     DTP_STAMP(3);
     __syncthreads();  // every wave is done with its staging rows
+    // this step's Adam scalars: requested now, consumed after the reduction
+    float2 adam_sc = make_float2(0.f, 1.f);
+    if constexpr (kAdam) adam_sc = sm.adam_tab[it % kAdamTab];
     {
       float* red = &sm.stage[0][0][0];
       const int q = lane >> 4, col = lane & 15;
@@ -318,6 +330,18 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
       a.loss_log[(size_t)lslot * a.n_models + model] = lg;
     }
+    // advance the sampler / loss-ring position and gather the next step's first
+    // chunk now: its index hashing and LDS reads overlap the optimizer's latency
+    if (!explicit_idx && ++bi == smp.steps_per_epoch) {
+      bi = 0;
+      ++epoch;
+      epoch_keys(smp, epoch, keys);
+    }
+    if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
+    if (it + 1 < a.n_steps) {
+      const BatchPos bpn = batch_at(epoch, bi);
+      nxt = gather(it + 1, bpn, keys, tid, bpn.size);
+    }
 
     if constexpr (MODE == DTP_MODE_GRAD) {
 #pragma unroll
@@ -328,33 +352,25 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       if (tid == 0) a.grad_out[(size_t)a.n_models * P + model] = mean_loss;
     } else {
       AdamScalars as = adam_consts(a.hp);
-      if constexpr (kAdam) {
-        const float2 sc = sm.adam_tab[it % kAdamTab];
-        as.step_size = sc.x;
-        as.bc2_sqrt = sc.y;
-      }
+      as.step_size = adam_sc.x;
+      as.bc2_sqrt = adam_sc.y;
       const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
+      // branch-free over the thread's NPT slots (slots past P hold zeros and store
+      // into sm.sink), so the compiler can interleave the slots' dependency chains
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        const int p = tid + k * kBlock;
-        if (p < P) {
-          if constexpr (kAdam) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
-          else sgd_update(pw[k], mr[k], g[k] * a.hp.grad_scale, lr, mom, wd, t == 0);
-          if (kScalarFwd) ws[pf[k]] = pw[k];
-          sm.wb[pfl[k]] = pw[k];
-          if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
-        }
+        if constexpr (kAdam) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
+        else sgd_update(pw[k], mr[k], g[k] * a.hp.grad_scale, lr, mom, wd, t == 0);
+      }
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const bool own = tid + k * kBlock < P;
+        if (kScalarFwd && own) ws[pf[k]] = pw[k];
+        *(own ? &sm.wb[pfl[k]] : &sm.sink[0]) = pw[k];
+        *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
       }
     }
     DTP_STAMP(6);
-    // advance the sampler / loss-ring position
-    if (!explicit_idx && ++bi == smp.steps_per_epoch) {
-      bi = 0;
-      ++epoch;
-      epoch_keys(smp, epoch, keys);
-      if (use_perm && it + 1 < a.n_steps) fill_perm(epoch);  // ordered by the barrier below
-    }
-    if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
     if (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight stores reached L2 before the barrier
     __syncthreads();  // updated weights visible; reduction tiles consumed
     DTP_STAMP(7);
