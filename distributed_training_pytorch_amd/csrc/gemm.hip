@@ -541,20 +541,53 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
     __syncthreads();
   }
 
-  // epilogue: acc[i][j][r] = C(row wr*128 + 16 i + 4 lg + r, col wc*64 + 16 j + lr)
+  // epilogue: acc[i][j][r] = C(row wr*128 + 16 i + 4 lg + r, col wc*64 + 16 j + lr).
+  // Per fragment row i, the 16 activation-gradient operands (aux) are requested
+  // together (clamped, unconditional loads) before any is used: 8 load round trips
+  // per lane instead of one per element.
   char* C = static_cast<char*>(a.C);
-  const char* aux = static_cast<const char*>(a.aux);
+  const uint16_t* aux = static_cast<const uint16_t*>(a.aux);
+  float bias[4];
+  int ncol[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wc * 64 + 16 * j + lr;
-    if (n >= a.N) continue;
-    const float bias = a.bias ? a.bias[n] : 0.f;
+    ncol[j] = n0 + wc * 64 + 16 * j + lr;
+    bias[j] = (a.bias && ncol[j] < a.N) ? a.bias[ncol[j]] : 0.f;
+  }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < 8; ++i) {
+    const int mrow = m0 + wr * 128 + 16 * i + 4 * lg;
+    float gate[4][4];
+    if (aux) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          gate[j][r] = bf16_to_f32(aux[static_cast<long long>(min(mrow + r, a.M - 1)) * a.ldaux + min(ncol[j], a.N - 1)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gate[j][r] = leaky_grad_from_out(gate[j][r], a.slope);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 128 + 16 * i + 4 * lg + r;
-        if (m < a.M) epilogue_store<DTP_DT_BF16>(a, C, aux, m, n, acc[i][j][r], bias);
+        const int m = mrow + r, n = ncol[j];
+        if (m >= a.M || n >= a.N) continue;
+        float v = a.alpha * acc[i][j][r] + bias[j];
+        if (aux) v *= gate[j][r];
+        if (a.act) v = leaky(v, a.slope);
+        const long long off = static_cast<long long>(m) * a.ldc + n;
+        if (a.out_dtype == DTP_DT_BF16) {
+          uint16_t* p = reinterpret_cast<uint16_t*>(C) + off;
+          if (a.accumulate) v += bf16_to_f32(*p);
+          *p = f32_to_bf16(v);
+        } else {
+          float* p = reinterpret_cast<float*>(C) + off;
+          if (a.accumulate) v += *p;
+          *p = v;
+        }
       }
     }
   }
@@ -595,6 +628,40 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* X, long long ld
     s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
     if (gridDim.y > 1) atomicAdd(out + n, s);
     else out[n] += s;
+  }
+}
+
+// bf16 column sums with 16-byte loads: a thread owns 8 adjacent columns, 32 threads
+// span 256 columns, 8 row groups x 128 rows per block (rows 16-byte aligned, N % 8 == 0)
+__global__ __launch_bounds__(256) void colsum_bf16x8_kernel(const void* X, long long ld, int M, int N, float* out) {
+  __shared__ float red[8][256];
+  const int cc = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int n0 = blockIdx.x * 256 + cc * 8;
+  const int r0 = blockIdx.y * 1024;
+  const int r1 = min(M, r0 + 1024);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n0 < N) {
+    const uint16_t* base = static_cast<const uint16_t*>(X) + n0;
+    for (int m = r0 + g; m < r1; m += 8) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + static_cast<long long>(m) * ld);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[2 * e] += __uint_as_float(w[e] << 16);
+        s[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[g][cc * 8 + e] = s[e];
+  __syncthreads();
+  const int c = threadIdx.x, n = blockIdx.x * 256 + c;
+  if (n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][c];
+    if (gridDim.y > 1) atomicAdd(out + n, t);
+    else out[n] += t;
   }
 }
 
@@ -681,6 +748,11 @@ extern "C" int dtp_colsum(const void* X, long long ld, int M, int N, int dtype, 
   if (!X || !out || M <= 0 || N <= 0) return set_err(1, "dtp_colsum: bad arguments");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
+  if (dtype == DTP_DT_BF16 && N % 8 == 0 && ld % 8 == 0 && aligned16(X)) {
+    hipLaunchKernelGGL(gemm::colsum_bf16x8_kernel, dim3((N + 255) / 256, (M + 1023) / 1024), dim3(256), 0, s, X, ld,
+                       M, N, out);
+    return check_launch("dtp_colsum(bf16x8)");
+  }
   const dim3 grid((N + 63) / 64, (M + 1023) / 1024), block(256);
   if (dtype == DTP_DT_BF16)
     hipLaunchKernelGGL((gemm::colsum_kernel<DTP_DT_BF16>), grid, block, 0, s, X, ld, M, N, out);

@@ -17,7 +17,25 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
   float* m = a.opt_m + (size_t)model * a.P;
   float* v = a.opt_v ? a.opt_v + (size_t)model * a.P : nullptr;
   const float* g = a.grad + (size_t)model * a.P;
-  if (a.kind == DTP_MODE_ADAM) {
+  // rows of 16-byte aligned float4s when every model row is (P % 4 == 0): 4 elements
+  // per thread and load (the update is HBM-bound: 28 B per parameter)
+  const bool vec = (a.P & 3) == 0 && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)g | (uintptr_t)(v ? v : p)) & 15) == 0;
+  if (a.kind == DTP_MODE_ADAM && vec) {
+    const AdamScalars s = adam_scalars(a.hp, t + 1);
+    const int P4 = a.P >> 2;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < P4; i += gridDim.x * kBlock) {
+      float4 w = reinterpret_cast<float4*>(p)[i], mi = reinterpret_cast<float4*>(m)[i];
+      float4 vi = reinterpret_cast<float4*>(v)[i];
+      const float4 gi = reinterpret_cast<const float4*>(g)[i];
+      adam_update(w.x, mi.x, vi.x, gi.x * a.hp.grad_scale, s);
+      adam_update(w.y, mi.y, vi.y, gi.y * a.hp.grad_scale, s);
+      adam_update(w.z, mi.z, vi.z, gi.z * a.hp.grad_scale, s);
+      adam_update(w.w, mi.w, vi.w, gi.w * a.hp.grad_scale, s);
+      reinterpret_cast<float4*>(p)[i] = w;
+      reinterpret_cast<float4*>(m)[i] = mi;
+      reinterpret_cast<float4*>(v)[i] = vi;
+    }
+  } else if (a.kind == DTP_MODE_ADAM) {
     const AdamScalars s = adam_scalars(a.hp, t + 1);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.P; i += gridDim.x * kBlock) {
       float w = p[i], mi = m[i], vi = v[i];

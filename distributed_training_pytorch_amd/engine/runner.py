@@ -83,6 +83,19 @@ def _geom(config, rank, world):
                            shuffle=True, distributed=config.dataloader == "distributed", seed=0)
 
 
+def _compute_dtype(config) -> torch.dtype:
+    return torch.bfloat16 if getattr(config, "precision", "fp32") == "bf16" else torch.float32
+
+
+def _fused_supported(config) -> bool:
+    from ..ops.mlp import MlpSpec
+
+    if _compute_dtype(config) != torch.float32:
+        return False
+    spec = MlpSpec(2, config.hidden, config.depth + 2, 4 if config.loss == "ce" else 1)
+    return spec.native_supported()
+
+
 def _optim(config) -> OptimConfig:
     return OptimConfig(config.optimizer, config.lr, momentum=config.momentum, weight_decay=config.weight_decay)
 
@@ -103,9 +116,16 @@ def train(config, env, device, rank, world, group: str = "base-demo") -> dict:
                           config={k: v for k, v in vars(config).items() if isinstance(v, (int, float, str, bool))})
     faults = FaultInjector(config.fail_at_iter, config.fail_rank, rank)
     t_start = time.perf_counter()
-    if config.engine == "fused":
+    engine = config.engine
+    if engine == "fused" and device.type == "cuda" and not _fused_supported(config):
+        # widths / dtypes the fused step kernel is not instantiated for train through
+        # nn.Modules whose Linears run on the MFMA GEMM (FlatDDP + FlatOptimizer)
+        rank_print(rank, f"fused step kernel has no instance for hidden={config.hidden} depth={config.depth} "
+                         f"precision={config.precision}: using the module engine (MFMA GEMM layers)")
+        engine = "module"
+    if engine == "fused":
         summary = _train_fused(config, device, rank, world, logger, faults)
-    elif config.engine == "module":
+    elif engine == "module":
         summary = _train_module(config, device, rank, world, logger, faults)
     else:
         summary = _train_stock(config, device, rank, world, logger, faults)
@@ -194,7 +214,8 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     idx_stream = EpochIndexStream(geom) if config.sampler == "torch" else None
     torch.manual_seed(config.seed)
     out_f = 4 if config.loss == "ce" else 1
-    bank = ModelBank(2, hidden=config.hidden, depth=config.depth, out_features=out_f).to(device)
+    bank = ModelBank(2, hidden=config.hidden, depth=config.depth, out_features=out_f,
+                     compute_dtype=_compute_dtype(config)).to(device)
     ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad,
                   comm=config.comm if config.comm in ("auto", "rccl", "xgmi") else "rccl")
     rank_print(rank, f"engine: module (FlatDDP over {ddp.comm})")

@@ -8,20 +8,26 @@ built for the fused HIP path.
   use.  The packing survives ``.to()/.cuda()`` (re-flattened in ``_apply``).
 * On a CUDA input the forward is ONE fused kernel and the backward ONE fused
   kernel (``ops.mlp.FusedMLPFunction``); on CPU it is plain PyTorch.
+* Widths the fused kernel does not cover (hidden > 15) run every Linear on the
+  MFMA GEMM with fused bias/LeakyReLU epilogues (``ops.gemm.mlp``), in fp32 or
+  with bf16 compute (``compute_dtype``; fp32 master weights and gradients).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
+from ..ops.gemm import mlp as gemm_mlp
 from ..ops.mlp import MlpSpec, fused_mlp
 
 
 class ToyModel(nn.Module):
     def __init__(self, in_features: int = 2, hidden: int = 10, depth: int = 3, out_features: int = 1,
-                 slope: float = 0.01):
+                 slope: float = 0.01, compute_dtype: torch.dtype = torch.float32):
         super().__init__()
         self.spec = MlpSpec(in_features, hidden, depth + 2, out_features, False, slope)
+        self.compute_dtype = compute_dtype
+        self._fused: bool | None = None
         mods: list[nn.Module] = [nn.Linear(in_features, hidden), nn.LeakyReLU(slope)]
         for _ in range(depth):
             mods += [nn.Linear(hidden, hidden), nn.LeakyReLU(slope)]
@@ -56,7 +62,15 @@ class ToyModel(nn.Module):
         with torch.no_grad():
             self._flat.copy_(flat.reshape(-1).to(self._flat))
 
+    def uses_fused_kernel(self) -> bool:
+        if self._fused is None:
+            self._fused = self.compute_dtype == torch.float32 and self.spec.native_supported()
+        return self._fused
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
-            return fused_mlp(x, self.spec, list(self.layers.parameters()))
+            if self.uses_fused_kernel():
+                return fused_mlp(x, self.spec, list(self.layers.parameters()))
+            lin = [m for m in self.layers if isinstance(m, nn.Linear)]
+            return gemm_mlp(x, [m.weight for m in lin], [m.bias for m in lin], self.spec.slope, self.compute_dtype)
         return self.layers(x)

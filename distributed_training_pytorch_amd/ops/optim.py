@@ -109,14 +109,17 @@ class FlatOptimizer:
         self.v = torch.zeros_like(self.params)
         self.step_ctr = torch.zeros(self.params.shape[0], dtype=torch.int32, device=self.params.device)
         n, P = self.params.shape
-        self._buf = torch.zeros(n * P + n, dtype=self.params.dtype, device=self.params.device)
+        self._buf = None if self.grad.is_contiguous() else \
+            torch.zeros(n * P + n, dtype=self.params.dtype, device=self.params.device)
         self.slope = slope
 
     @torch.no_grad()
     def step(self) -> None:
+        # the kernel reads grad[i*P : (i+1)*P] only (the loss slots behind them are
+        # read only with a loss log), so a contiguous [n, P] gradient is used in place
         n, P = self.params.shape
-        if self.grad.is_contiguous() and self.grad.data_ptr() == self._buf.data_ptr():
-            buf = self._buf
+        if self.grad.is_contiguous() and self.grad.device == self.params.device:
+            buf = self.grad.view(-1)
         else:
             self._buf[: n * P].copy_(self.grad.reshape(-1))
             buf = self._buf
