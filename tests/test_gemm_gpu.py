@@ -64,19 +64,20 @@ def test_gemm_bf16_big_tile_kernel(ta, tb):
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192)])
-def test_gemm_bf16_fast_kernel(ta, tb, shape):
+@pytest.mark.parametrize("kernel", [True, 6])  # default schedule, 4-slot ring (fast = 2 + variant 4)
+def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     """The LDS-DMA 256x256 kernel (row images + transposing LDS reads): every layout,
     ragged M/N edges, bias / LeakyReLU' (aux) epilogues, f32 and bf16 outputs."""
     M, N, K = shape
     a, b = _ops(M, N, K, ta, tb, torch.bfloat16, 11)
     bias = torch.randn(N, device=DEV)
     ref = _ref(a, b, ta, tb)
-    c = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1, bias=bias, fast=True)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1, bias=bias, fast=kernel)
     torch.testing.assert_close(c, ref + bias, rtol=1e-4, atol=2e-3 * K ** 0.5)
     classic = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1, bias=bias, fast=False)
     torch.testing.assert_close(c, classic, rtol=1e-4, atol=2e-3 * K ** 0.5)
     aux = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    cb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, aux=aux, slope=0.1, fast=True)
+    cb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, aux=aux, slope=0.1, fast=kernel)
     torch.testing.assert_close(cb.float(), ref * torch.where(aux.float() > 0, 1.0, 0.1), rtol=1e-2, atol=5e-2)
 
 
