@@ -520,131 +520,6 @@ DTP_DEV void fast_epilogue(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], int m
   }
 }
 
-// ---------------------------------------------------------------------------
-// Ring variant of the LDS-DMA kernel: the K loop runs in PHASES of 32 k (one
-// 16x16x32 MFMA depth; 32 MFMAs per wave), each phase's operands in one of FOUR
-// 32 KiB LDS slots, the DMA of phase q+3 issued at phase q.  Phase q waits only
-// for its own slot with a COUNTED vmcnt (phases q+1, q+2 stay in flight across
-// the raw s_barrier) -- no vmcnt(0) drain per K-tile as in the two-buffer form.
-//   RAW: slot q was filled by DMA(q) issued 3 phases earlier; every wave waits
-//        vmcnt(8) (its own DMA(q) pieces retired), then the barrier.
-//   WAR: DMA(q+3) goes to slot (q-1) & 3, issued after the barrier that follows
-//        every wave's phase q-1 reads (their MFMAs consumed them).
-// Row images have 64-byte rows here; fsw64(r) = ((r >> 3) & 1) << 1 keeps the
-// 16x16x32 fragment reads conflict-free for the ds_read_b128 lane groups.
-// ---------------------------------------------------------------------------
-constexpr int kRingSlot = 256 * 32 * 2;  // bytes of one operand's image per slot (32 k)
-
-DTP_DEV int fsw64(int r) { return ((r >> 3) & 1) << 1; }
-
-template <bool TRANS>
-DTP_DEV void ring_sources(const char* (&src)[2], const char* base, long long ld, int r0, int R, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    if constexpr (!TRANS) {  // 16 rows x 64 B per instruction: row (8i+w)*16 + lane/4, chunk lane%4
-      const int row = (8 * i + wave) * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ fsw64(row);
-      const int rr = min(r0 + row, R - 1);
-      src[i] = base + (static_cast<long long>(rr) * ld + c * 8) * 2;
-    } else {  // 2 k-rows x 512 B per instruction
-      const int k = (8 * i + wave) * 2 + (lane >> 5);
-      const int c = (lane & 31) ^ (fswz(k) << 1);
-      const int col = min(r0 + c * 8, R - 8);
-      src[i] = base + (static_cast<long long>(k) * ld + col) * 2;
-    }
-  }
-}
-
-template <bool TRANS, int NF>
-DTP_DEV void ring_offsets(int (&off)[TRANS ? NF : 1], int rb, int lane) {
-  const int lr = lane & 15, lg = lane >> 4;
-  if constexpr (!TRANS) {
-    off[0] = (rb + lr) * 64 + ((lg ^ fsw64(lr)) << 4);
-  } else {
-    const int q = lr >> 2, p = lr & 3, sw = q | ((lg & 1) << 2);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) off[f] = (8 * lg + q) * 512 + (((rb + 16 * f) * 2) ^ (sw << 5)) + 8 * p;
-  }
-}
-
-template <bool TRANS>
-DTP_DEV bf16x8 ring_frag(const char* img, const int* off, int f) {
-  if constexpr (!TRANS) {
-    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + off[0] + f * 1024));
-  } else {
-    const char* p = img + off[f];
-    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p));
-    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 2048));
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  }
-}
-
-DTP_DEV void ring_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <bool TA, bool TB>
-__global__ __launch_bounds__(kFastThreads) void gemm_ring_kernel(DtpGemmArgs a) {
-  constexpr int BM = 256, BN = 256;
-  __shared__ __align__(16) char lds[4 * 2 * kRingSlot];  // [slot][A | B]: 128 KiB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3, lr = lane & 15, lg = lane >> 4;
-  const TileId id = decode_tile<BM, BN>(a);
-  const int m0 = id.m0, n0 = id.n0, nq = a.K / 32;
-
-  const char* srcA[2];
-  const char* srcB[2];
-  ring_sources<TA>(srcA, static_cast<const char*>(a.A), a.lda, m0, a.M, wave, lane);
-  ring_sources<TB>(srcB, static_cast<const char*>(a.B), a.ldb, n0, a.N, wave, lane);
-  const long long qbA = TA ? 32LL * a.lda * 2 : 64, qbB = TB ? 32LL * a.ldb * 2 : 64;
-  auto dma = [&](int q) {  // phase q's operands -> slot q & 3 (4 pieces per thread)
-    char* img = lds + (q & 3) * 2 * kRingSlot;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcA[i] + q * qbA), (lds_void_t*)(img + (8 * i + wave) * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[i] + q * qbB),
-                                       (lds_void_t*)(img + kRingSlot + (8 * i + wave) * 1024), 16, 0, 0);
-    }
-  };
-  int offA[TA ? 8 : 1], offB[TB ? 4 : 1];
-  ring_offsets<TA, 8>(offA, wr * 128, lane);
-  ring_offsets<TB, 4>(offB, wc * 64, lane);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int q = 0; q < 3 && q < nq; ++q) dma(q);
-  for (int q = 0; q < nq; ++q) {
-    if (q + 2 < nq) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (q + 1 < nq) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ring_barrier();
-    if (q + 3 < nq) dma(q + 3);
-    const char* ia = lds + (q & 3) * 2 * kRingSlot;
-    const char* ib = ia + kRingSlot;
-    bf16x8 fa[8], fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = ring_frag<TB>(ib, offB, j);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = ring_frag<TA>(ia, offA, i);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    // every fragment read first (one LDS latency per phase), then the 32 MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, (TA ? 16 : 8) + (TB ? 8 : 4), 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
-  }
-  fast_epilogue(a, acc, m0, n0, wr, wc, lr, lg);
-}
-
 // VAR (schedule experiments, selected by DtpGemmArgs::fast = 2 + VAR): bit 0 = static
 // s_setprio(1) for waves 4-7 instead of per-cluster flips; bit 1 = the next tile's
 // DMA split over the two k-steps (4 pieces ahead of each MFMA cluster)
@@ -723,23 +598,8 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
   fast_epilogue(a, acc, m0, n0, wr, wc, lr, lg);
 }
 
-template <bool TA, bool TB>
-int launch_ring_t(const DtpGemmArgs& a, hipStream_t s) {
-  const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_ring_kernel<TA, TB>), dim3((unsigned)tiles), dim3(kFastThreads), 0, s, a);
-  return check_launch("dtp_gemm(LDS-DMA ring 256x256)");
-}
-
-inline int launch_ring(const DtpGemmArgs& a, hipStream_t s) {
-  switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
-    case 0: return launch_ring_t<false, false>(a, s);
-    case 1: return launch_ring_t<false, true>(a, s);
-    case 2: return launch_ring_t<true, false>(a, s);
-    default: return launch_ring_t<true, true>(a, s);
-  }
-}
-
-constexpr int kFastDefaultVar = 2;  // next tile's DMA split over the k-steps: +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl)
+constexpr int kFastDefaultVar = 2;  // next tile's DMA split over the k-steps: +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl; the ring schedules
+                                     // measured there live on branch exp/gemm-ring)
 
 template <int VAR>
 int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
@@ -848,8 +708,7 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   const bool fast_shape = a.dtype == DTP_DT_BF16 && a.splitk == 1 && a.K % 64 == 0 && a.vec_a && a.vec_b &&
                           (!a.trans_a || a.M % 8 == 0) && (!a.trans_b || a.N % 8 == 0) && !a.force_big;
   if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
-    const int var = a.fast >= 2 ? a.fast - 2 : gemm::kFastDefaultVar;
-    if (var >= 4) return gemm::launch_ring(a, s);
+    const int var = a.fast >= 2 ? (a.fast - 2) & 3 : gemm::kFastDefaultVar;
     switch (var) {
       case 0: return gemm::launch_fast<0>(a, s);
       case 1: return gemm::launch_fast<1>(a, s);

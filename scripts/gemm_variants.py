@@ -25,7 +25,7 @@ def t_ms(fn, iters=10):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    variants = ["var1", "var2", "var4", "torch"]  # var4 = 4-slot ring
+    variants = ["var0", "var1", "var2", "var3", "torch"]
     for (M, N, K, lay) in [(4096, 4096, 4096, "NN"), (8192, 8192, 8192, "NN"), (8192, 8192, 8192, "TT"),
                            (8192, 8192, 8192, "NT")]:
         ta, tb = lay[0] == "T", lay[1] == "T"

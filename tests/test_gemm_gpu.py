@@ -64,7 +64,7 @@ def test_gemm_bf16_big_tile_kernel(ta, tb):
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192)])
-@pytest.mark.parametrize("kernel", [True, 6])  # default schedule, 4-slot ring (fast = 2 + variant 4)
+@pytest.mark.parametrize("kernel", [True, 2, 3])  # default schedule, variants 0 and 1 (fast = 2 + variant)
 def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     """The LDS-DMA 256x256 kernel (row images + transposing LDS reads): every layout,
     ragged M/N edges, bias / LeakyReLU' (aux) epilogues, f32 and bf16 outputs."""
