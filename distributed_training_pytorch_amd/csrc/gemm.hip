@@ -614,6 +614,89 @@ int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
   return check_launch("dtp_gemm(LDS-DMA 256x256)");
 }
 
+
+// Skinny-K GEMM (K <= 16): an outer-product-like layer (the first Linear of an MLP,
+// K = in_features, and the input gradient of the last one, K = out_features) is
+// pure output bandwidth -- write C (and read aux) in 16-byte vectors instead of
+// running a 128x128 MFMA tile with 1/16th of its K used.  Block = 16 rows x 256
+// columns; thread t owns columns 8 (t & 31) .. +8 of rows 2 (t >> 5) .. +2.
+template <int DT, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
+  __shared__ float sa[16][17];
+  __shared__ float sb[256][17];
+  const int tid = threadIdx.x;
+  const int n0 = blockIdx.x * 256, m0 = blockIdx.y * 16;
+  const char* A = static_cast<const char*>(a.A);
+  const char* B = static_cast<const char*>(a.B);
+  constexpr int ES = Ty<DT>::ES;
+  for (int e = tid; e < 16 * 16; e += 256) {
+    const int r = e >> 4, k = e & 15, m = m0 + r;
+    float v = 0.f;
+    if (m < a.M && k < a.K) v = load_elem<DT>(A + (TA ? (long long)k * a.lda + m : (long long)m * a.lda + k) * ES);
+    sa[r][k] = v;
+  }
+  for (int e = tid; e < 256 * 16; e += 256) {
+    const int c = e >> 4, k = e & 15, n = n0 + c;
+    float v = 0.f;
+    if (n < a.N && k < a.K) v = load_elem<DT>(B + (TB ? (long long)k * a.ldb + n : (long long)n * a.ldb + k) * ES);
+    sb[c][k] = v;
+  }
+  __syncthreads();
+  const int cc = (tid & 31) * 8, rr = (tid >> 5) * 2;
+  float bias[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bias[c] = (a.bias && n0 + cc + c < a.N) ? a.bias[n0 + cc + c] : 0.f;
+  char* C = static_cast<char*>(a.C);
+  const char* aux = static_cast<const char*>(a.aux);
+  const bool vec_c = (a.ldc % 8 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) && n0 + cc + 8 <= a.N;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int m = m0 + rr + r;
+    if (m >= a.M) continue;
+    float acc[8], v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float t = 0.f;
+      for (int k = 0; k < a.K; ++k) t = fmaf(sa[rr + r][k], sb[cc + c][k], t);
+      acc[c] = t;
+      v[c] = a.alpha * t + bias[c];
+    }
+    if (vec_c && a.out_dtype == DTP_DT_BF16 && !a.accumulate) {
+      if (aux) {
+        const uint4 g = *reinterpret_cast<const uint4*>(aux + ((long long)m * a.ldaux + n0 + cc) * ES);
+        float gv[8];
+        if constexpr (DT == DTP_DT_BF16) {
+          const uint32_t w[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            gv[2 * q] = __uint_as_float(w[q] << 16);
+            gv[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) gv[c] = load_elem<DT>(aux + ((long long)m * a.ldaux + n0 + cc + c) * ES);
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] *= leaky_grad_from_out(gv[c], a.slope);
+      }
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float x0 = a.act ? leaky(v[2 * q], a.slope) : v[2 * q];
+        const float x1 = a.act ? leaky(v[2 * q + 1], a.slope) : v[2 * q + 1];
+        o[q] = uint32_t(f32_to_bf16(x0)) | (uint32_t(f32_to_bf16(x1)) << 16);
+      }
+      *reinterpret_cast<uint4*>(C + ((long long)m * a.ldc + n0 + cc) * 2) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int n = n0 + cc + c;
+        if (n < a.N) epilogue_store<DT>(a, C, aux, m, n, acc[c], bias[c]);
+      }
+    }
+  }
+}
+
 // out[n] (+)= sum_m X[m*ld + n]: bias gradients.  64 columns x 4 row groups per block,
 // 1024 rows per block; partial sums of several row blocks meet in f32 atomics.
 template <int DT>
@@ -699,6 +782,22 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   if (a.splitk > 1 && !a.accumulate) {  // atomics accumulate into C: clear it first
     hipError_t e = hipMemset2DAsync(a.C, sizeof(float) * static_cast<size_t>(a.ldc), 0, sizeof(float) * a.N, a.M, s);
     if (e != hipSuccess) return set_err(2, "dtp_gemm: clearing the split-K output failed");
+  }
+  // K <= 16 (an MLP's first layer / last layer's input gradient): output-bandwidth kernel
+  if (a.K <= 16 && a.splitk == 1) {
+    const dim3 gs((a.N + 255) / 256, (a.M + 15) / 16), bs(256);
+    const int k3 = (a.dtype == DTP_DT_BF16 ? 4 : 0) | (a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0);
+    switch (k3) {
+      case 0: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, false, false>), gs, bs, 0, s, a); break;
+      case 1: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, false, true>), gs, bs, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, true, false>), gs, bs, 0, s, a); break;
+      case 3: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, true, true>), gs, bs, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, false>), gs, bs, 0, s, a); break;
+      case 5: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, true>), gs, bs, 0, s, a); break;
+      case 6: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, true, false>), gs, bs, 0, s, a); break;
+      default: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, true, true>), gs, bs, 0, s, a); break;
+    }
+    return check_launch("dtp_gemm(skinny K)");
   }
   // big bf16 problems (>= 256 tiles of 256x256, no split-K): the 256x256 kernel
   const long long big_tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);

@@ -81,6 +81,28 @@ def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     torch.testing.assert_close(cb.float(), ref * torch.where(aux.float() > 0, 1.0, 0.1), rtol=1e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("K", [1, 2, 13])
+def test_gemm_skinny_k(ta, tb, K):
+    """K <= 16 (first layer / last layer's input gradient): the output-bandwidth kernel,
+    vector bf16 stores with bias, LeakyReLU'(aux) and LeakyReLU epilogues, ragged edges."""
+    M, N = 1000, 1032
+    a, b = _ops(M, N, K, ta, tb, torch.bfloat16, 5)
+    bias = torch.randn(N, device=DEV)
+    ref = _ref(a, b, ta, tb)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, bias=bias, alpha=0.5)
+    torch.testing.assert_close(c, 0.5 * ref + bias, rtol=1e-5, atol=1e-4)
+    aux = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    cb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, aux=aux, slope=0.1)
+    torch.testing.assert_close(cb.float(), ref * torch.where(aux.float() > 0, 1.0, 0.1), rtol=1e-2, atol=2e-2)
+    ca = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, bias=bias, act=True, slope=0.1)
+    torch.testing.assert_close(ca.float(), torch.nn.functional.leaky_relu(ref + bias, 0.1), rtol=1e-2, atol=2e-2)
+    af, bf = a.float(), b.float()
+    cf = gemm(af, bf, trans_a=ta, trans_b=tb, bias=bias, act=True, slope=0.1)
+    torch.testing.assert_close(cf, torch.nn.functional.leaky_relu(ref + bias, 0.1), rtol=1e-5, atol=1e-4)
+
+
 def test_gemm_epilogues():
     M, N, K = 300, 200, 96
     a, b = _ops(M, N, K, False, False, torch.float32, 1)
