@@ -76,7 +76,7 @@ template <class S, int MODE, bool PROF = false>
 __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT;
-  static_assert(kWaves * NT * 256 <= kWaves * 2 * 2 * kStgArr, "reduction tiles must fit in the staging area");
+  static_assert(NT * 256 <= 2 * 2 * kStgArr, "a wave's reduction tiles must fit in its staging area");
   __shared__ __align__(16) TrainSmem<S> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
@@ -282,39 +282,40 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     }
     DTP_STAMP(8 + wave);
     DTP_STAMP(3);
-    __syncthreads();  // every wave is done with its staging rows
-    // this step's Adam scalars: requested now, consumed after the reduction
-    float2 adam_sc = make_float2(0.f, 1.f);
-    if constexpr (kAdam) adam_sc = sm.adam_tab[it % kAdamTab];
+    // each wave parks its partial dW tiles in its OWN staging area (no other wave
+    // touches it, and this wave's staging reads were issued before these writes),
+    // so one barrier publishes them
     {
-      float* red = &sm.stage[0][0][0];
       const int q = lane >> 4, col = lane & 15;
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        float* tl = red + (wave * NT + tt) * 256;
+        float* tl = &sm.stage[wave][0][0] + tt * 256;
 #pragma unroll
         for (int r = 0; r < 4; ++r) tl[(4 * q + r) * 16 + col] = acc[tt][r];
       }
     }
     __syncthreads();
+    // this step's Adam scalars: requested now, consumed after the reduction
+    float2 adam_sc = make_float2(0.f, 1.f);
+    if constexpr (kAdam) adam_sc = sm.adam_tab[it % kAdamTab];
     // no wave loads this step's weights any more: drop them from the scalar cache
     // before the optimizer writes the new ones (mlp_scalar.h protocol)
     if (kScalarFwd && wave == 0) __builtin_amdgcn_s_dcache_inv();
     DTP_STAMP(4);
 
-    const float* red = &sm.stage[0][0][0];
     float g[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int tt = tp[k] >> 8, e = tp[k] & 255;
       float s = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) s += red[(ww * NT + tt) * 256 + e];
+      for (int ww = 0; ww < kWaves; ++ww) s += sm.stage[ww][0][tt * 256 + e];
       g[k] = s;
     }
     float lsum = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) lsum += red[(ww * NT + SC::tile(NL - 1)) * 256 + SC::lossrow() * 16 + SC::losscol()];
+    for (int ww = 0; ww < kWaves; ++ww)
+      lsum += sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
     const float mean_loss = lsum * inv;
     DTP_STAMP(5);
 
