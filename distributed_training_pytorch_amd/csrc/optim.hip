@@ -79,7 +79,9 @@ extern "C" int dtp_flat_optimizer(const DtpOptArgs* a, void* stream) {
   if (!a || a->P <= 0 || a->n_models <= 0) return -1;
   if (a->kind != DTP_MODE_ADAM && a->kind != DTP_MODE_SGD) return -2;
   hipStream_t st = (hipStream_t)stream;
-  int nblk = (a->P + dtp::kBlock - 1) / dtp::kBlock;
+  // small models (the toy's 371 parameters): one block per model loops over its
+  // parameters and advances the step counter itself -- no follow-up launch
+  int nblk = a->P <= 16 * dtp::kBlock ? 1 : (a->P + dtp::kBlock - 1) / dtp::kBlock;
   if (nblk > 1024) nblk = 1024;
   dim3 grid(nblk, a->n_models), block(dtp::kBlock);
   hipLaunchKernelGGL(dtp::flat_optimizer_kernel, grid, block, 0, st, *a);

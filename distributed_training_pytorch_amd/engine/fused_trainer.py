@@ -221,8 +221,12 @@ class FusedTrainer:
                 self._reference_step()
             return
         if self.comm in ("rccl", "host"):
-            for _ in range(n_steps):
-                self._rccl_step()
+            remaining = n_steps
+            G = max(1, min(self.cfg.steps_per_launch, 64))
+            while remaining > 0:
+                k = G if remaining >= G else 1
+                self._rccl_steps(k)
+                remaining -= k
             return
         remaining = n_steps
         while remaining > 0:
@@ -283,21 +287,35 @@ class FusedTrainer:
         self._launch(k, idx, b0)
         self._keepalive = idx
 
-    def _rccl_step(self):
+    def _rccl_steps(self, k: int):
+        """k iterations of grad kernel -> RCCL all-reduce -> flat optimizer; with
+        rccl_graph, all k captured in ONE hipGraph (one host replay per k steps: a
+        replay costs ~10 us of host time, more than the step itself)."""
         lib = nat.load()
+        if self.cfg.sampler == "torch":
+            # exact DistributedSampler order: host-built indices, one eager step each
+            for _ in range(k):
+                b = self.geom.batch_size_at(self.t)
+                idx = torch.tensor([self._idx_stream.indices(self.t)], dtype=torch.int32).pin_memory()
+                idx = idx.to(self.device, non_blocking=True)
+                self._rccl_body(lib, idx, b)
+                self._keepalive = idx
+                self.t += 1
+            return
         if self.cfg.rccl_graph and self.comm == "rccl":
-            g = self._graphs.get("rccl")
+            g = self._graphs.get(("rccl", k))
             if g is None:
-                g = self._capture_rccl()
+                g = self._capture_rccl(k)
             if g is not False:
                 g.replay()
-                self.t += 1
+                self.t += k
                 return
-        self._rccl_body(lib)
-        self.t += 1
+        for _ in range(k):
+            self._rccl_body(lib)
+            self.t += 1
 
-    def _rccl_body(self, lib, idx=None):
-        a = self._train_args(1, nat.MODE_GRAD, idx)
+    def _rccl_body(self, lib, idx=None, batch_override=None):
+        a = self._train_args(1, nat.MODE_GRAD, idx, batch_override)
         nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
                   "dtp_mlp_train(grad)")
         comm_util.all_reduce_(self.comm_buf, self.group)
@@ -305,7 +323,7 @@ class FusedTrainer:
                             grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world,
                             slope=self.spec.slope)
 
-    def _capture_rccl(self):
+    def _capture_rccl(self, k: int = 1):
         lib = nat.load()
         try:
             s = torch.cuda.Stream(device=self.device)
@@ -317,13 +335,14 @@ class FusedTrainer:
             s.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                self._rccl_body(lib)
+                for _ in range(k):
+                    self._rccl_body(lib)
             torch.cuda.current_stream().wait_stream(s)
-            self._graphs["rccl"] = g
+            self._graphs[("rccl", k)] = g
             return g
         except Exception as e:  # capture of collectives unsupported -> eager
             print(f"[dtp] hipGraph capture of the RCCL step failed ({e}); running eager", flush=True)
-            self._graphs["rccl"] = False
+            self._graphs[("rccl", k)] = False
             return False
 
     # ------------------------------------------------------------------ CPU reference path

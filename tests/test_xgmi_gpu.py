@@ -19,14 +19,14 @@ pytestmark = pytest.mark.gpu
 STEPS = 9
 
 
-def _gpu_rank(rank, world, comm, steps, launch):
+def _gpu_rank(rank, world, comm, steps, launch, sampler="device"):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ds = ToyData(n=512, seed=1)
     X, Y = ds.device_tensors(dev)
     geom = SamplerGeometry(n=512, world=world, rank=rank, batch=128, seed=3)
     tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-2),
-                      EngineConfig(comm=comm, launch=launch, steps_per_launch=4), init_params=_init(100 + rank))
+                      EngineConfig(comm=comm, launch=launch, steps_per_launch=4, sampler=sampler), init_params=_init(100 + rank))
     tr.train(steps)
     tr.synchronize()
     out = (tr.params.cpu(), tr.losses(0, steps), tr.comm)
@@ -53,6 +53,17 @@ def test_rccl_step_path_single_rank():
     assert used == "rccl"
     torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=2e-5)
     torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
+
+
+def test_rccl_step_path_torch_sampler_matches_fused():
+    """RCCL path with the exact DistributedSampler order (host-built indices per
+    step) equals the fused single-rank path fed the same explicit indices; 9 steps
+    over a 512-sample / batch-128 epoch cross an epoch boundary."""
+    a = run_ranks(_gpu_rank, 1, ("rccl", STEPS, "persistent", "torch"), timeout=300, backend="nccl")
+    b = run_ranks(_gpu_rank, 1, ("auto", STEPS, "persistent", "torch"), timeout=300, backend="nccl")
+    assert a[0][2] == "rccl"
+    torch.testing.assert_close(a[0][0], b[0][0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a[0][1], b[0][1], rtol=1e-5, atol=1e-6)
 
 
 def _ar_rank(rank, world, n, calls):
