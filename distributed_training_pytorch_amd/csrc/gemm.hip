@@ -520,13 +520,153 @@ DTP_DEV void fast_epilogue(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], int m
   }
 }
 
+// LDS-staged epilogue of the 256x256 LDS-DMA kernel (the operand images are dead
+// once the K loop ends).  The MFMA layout gives a lane one column and 4 rows per
+// fragment, so a direct store writes 2-4 bytes per lane and the aux / accumulate
+// operands come back one scalar load at a time.  Instead each wave parks its
+// 128x64 f32 sub-tile in its own LDS region, 64 rows per pass (row stride 68
+// floats: the ds_write_b32 of one fragment register hits 64 distinct banks), and
+// reads it back row-major: lane L owns 8 adjacent columns 8 (L & 7) .. +8 of rows
+// L / 8 + 8 t, so aux, the old C (accumulate) and C itself move as 16-byte vectors
+// (8 lanes = one 128-byte bf16 row segment).  Columns past N (ragged last tile) or
+// unaligned operands take the per-element path.
+constexpr int kEpiStride = 68;
+constexpr int kEpiWaveFloats = 64 * kEpiStride;
+
+DTP_DEV void bf16x8_to_f32(const uint4& g, float (&x)[8]) {
+  const uint32_t w[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    x[2 * q] = __uint_as_float(w[q] << 16);
+    x[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+
+// one pass = fragment rows 4H .. 4H+3 (H a template parameter: acc is indexed
+// statically, so it stays in registers)
+template <int H>
+DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], float* buf, const float (&bias)[8],
+                                int m0, int wr, int ncol, bool vec, int lane) {
+  const int lr = lane & 15, lg = lane >> 4, c8 = lane & 7, rl = lane >> 3;
+  char* C = static_cast<char*>(a.C);
+  const uint16_t* aux = static_cast<const uint16_t*>(a.aux);
+  const bool bf16_out = a.out_dtype == DTP_DT_BF16;
+  constexpr int h = H;
+  {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) buf[(16 * ii + 4 * lg + r) * kEpiStride + 16 * j + lr] = acc[4 * h + ii][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's stores land before its own reads (LDS is in order per wave)
+#pragma unroll
+    for (int t0 = 0; t0 < 8; t0 += 4) {
+      float v[4][8];
+      int mrow[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int lrow = rl + 8 * (t0 + u);
+        mrow[u] = m0 + wr * 128 + 64 * h + lrow;
+        const float4 x0 = *reinterpret_cast<const float4*>(buf + lrow * kEpiStride + 8 * c8);
+        const float4 x1 = *reinterpret_cast<const float4*>(buf + lrow * kEpiStride + 8 * c8 + 4);
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[u][c] = xs[c];
+      }
+      if (vec) {
+        // every operand of the 4 rows requested before any is used (rows past M clamped, never stored)
+        uint4 g[4], oc[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const long long mr = min(mrow[u], a.M - 1);
+          if (aux) g[u] = *reinterpret_cast<const uint4*>(aux + mr * a.ldaux + ncol);
+          if (a.accumulate) {
+            if (bf16_out) {
+              oc[u][0] = *reinterpret_cast<const uint4*>(C + (mr * a.ldc + ncol) * 2);
+            } else {
+              oc[u][0] = *reinterpret_cast<const uint4*>(C + (mr * a.ldc + ncol) * 4);
+              oc[u][1] = *reinterpret_cast<const uint4*>(C + (mr * a.ldc + ncol + 4) * 4);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float y[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) y[c] = a.alpha * v[u][c] + bias[c];
+          if (aux) {
+            float gv[8];
+            bf16x8_to_f32(g[u], gv);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) y[c] *= leaky_grad_from_out(gv[c], a.slope);
+          }
+          if (a.act) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) y[c] = leaky(y[c], a.slope);
+          }
+          if (mrow[u] >= a.M) continue;
+          const long long off = static_cast<long long>(mrow[u]) * a.ldc + ncol;
+          if (bf16_out) {
+            if (a.accumulate) {
+              float ov[8];
+              bf16x8_to_f32(oc[u][0], ov);
+#pragma unroll
+              for (int c = 0; c < 8; ++c) y[c] += ov[c];
+            }
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = uint32_t(f32_to_bf16(y[2 * q])) | (uint32_t(f32_to_bf16(y[2 * q + 1])) << 16);
+            *reinterpret_cast<uint4*>(C + off * 2) = make_uint4(o[0], o[1], o[2], o[3]);
+          } else {
+            if (a.accumulate) {
+              const uint32_t w[8] = {oc[u][0].x, oc[u][0].y, oc[u][0].z, oc[u][0].w,
+                                     oc[u][1].x, oc[u][1].y, oc[u][1].z, oc[u][1].w};
+#pragma unroll
+              for (int c = 0; c < 8; ++c) y[c] += __uint_as_float(w[c]);
+            }
+            *reinterpret_cast<float4*>(C + off * 4) = make_float4(y[0], y[1], y[2], y[3]);
+            *reinterpret_cast<float4*>(C + (off + 4) * 4) = make_float4(y[4], y[5], y[6], y[7]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (mrow[u] >= a.M) continue;
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (ncol + c < a.N)
+              epilogue_store<DTP_DT_BF16>(a, C, static_cast<const char*>(a.aux), mrow[u], ncol + c, v[u][c], bias[c]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this pass done before the next pass overwrites
+  }
+}
+
+DTP_DEV void fast_epilogue_lds(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], char* lds, int m0, int n0, int wave,
+                               int wr, int wc, int lane) {
+  float* buf = reinterpret_cast<float*>(lds) + wave * kEpiWaveFloats;
+  const int ncol = n0 + wc * 64 + 8 * (lane & 7);
+  const uintptr_t cp = reinterpret_cast<uintptr_t>(a.C), ap = reinterpret_cast<uintptr_t>(a.aux);
+  const bool vec = ncol + 8 <= a.N && a.ldc % 8 == 0 && (cp & 15) == 0 && (!a.aux || (a.ldaux % 8 == 0 && (ap & 15) == 0));
+  float bias[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bias[c] = (a.bias && ncol + c < a.N) ? a.bias[ncol + c] : 0.f;
+  fast_epilogue_pass<0>(a, acc, buf, bias, m0, wr, ncol, vec, lane);
+  fast_epilogue_pass<1>(a, acc, buf, bias, m0, wr, ncol, vec, lane);
+}
+
 // VAR (schedule experiments, selected by DtpGemmArgs::fast = 2 + VAR): bit 0 = static
 // s_setprio(1) for waves 4-7 instead of per-cluster flips; bit 1 = the next tile's
-// DMA split over the two k-steps (4 pieces ahead of each MFMA cluster)
+// DMA split over the two k-steps (4 pieces ahead of each MFMA cluster); bit 2 = the
+// direct per-element epilogue instead of the LDS-staged one
 template <bool TA, bool TB, int VAR>
 __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64;
-  __shared__ __align__(16) char lds[2 * 2 * kFastImg];  // [buffer][A | B] images: 128 KiB
+  // [buffer][A | B] images: 128 KiB; after the K loop, 8 waves x 64 x 68 f32 epilogue staging (136 KiB)
+  constexpr int kLdsBytes = 2 * 2 * kFastImg > 8 * kEpiWaveFloats * 4 ? 2 * 2 * kFastImg : 8 * kEpiWaveFloats * 4;
+  __shared__ __align__(16) char lds[kLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3, lr = lane & 15, lg = lane >> 4;
   const TileId id = decode_tile<BM, BN>(a);
@@ -595,7 +735,8 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
     __syncthreads();
   }
 
-  fast_epilogue(a, acc, m0, n0, wr, wc, lr, lg);
+  if constexpr (VAR & 4) fast_epilogue(a, acc, m0, n0, wr, wc, lr, lg);  // direct per-element stores (A/B)
+  else fast_epilogue_lds(a, acc, lds, m0, n0, wave, wr, wc, lane);
 }
 
 constexpr int kFastDefaultVar = 2;  // next tile's DMA split over the k-steps: +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl; the ring schedules
@@ -618,18 +759,20 @@ int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
 // Skinny-K GEMM (K <= 16): an outer-product-like layer (the first Linear of an MLP,
 // K = in_features, and the input gradient of the last one, K = out_features) is
 // pure output bandwidth -- write C (and read aux) in 16-byte vectors instead of
-// running a 128x128 MFMA tile with 1/16th of its K used.  Block = 16 rows x 256
-// columns; thread t owns columns 8 (t & 31) .. +8 of rows 2 (t >> 5) .. +2.
+// running a 128x128 MFMA tile with 1/16th of its K used.  Block = kSkinnyRows rows x
+// 256 columns (the B block staged once per 128 rows, not per 16); thread t owns
+// columns 8 (t & 31) .. +8 of rows 2 (t >> 5) + 16 q .. +2, q < kSkinnyRows / 16.
+constexpr int kSkinnyRows = 128;
 template <int DT, bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
-  __shared__ float sa[16][17];
+  __shared__ float sa[kSkinnyRows][17];
   __shared__ float sb[256][17];
   const int tid = threadIdx.x;
-  const int n0 = blockIdx.x * 256, m0 = blockIdx.y * 16;
+  const int n0 = blockIdx.x * 256, m0 = blockIdx.y * kSkinnyRows;
   const char* A = static_cast<const char*>(a.A);
   const char* B = static_cast<const char*>(a.B);
   constexpr int ES = Ty<DT>::ES;
-  for (int e = tid; e < 16 * 16; e += 256) {
+  for (int e = tid; e < kSkinnyRows * 16; e += 256) {
     const int r = e >> 4, k = e & 15, m = m0 + r;
     float v = 0.f;
     if (m < a.M && k < a.K) v = load_elem<DT>(A + (TA ? (long long)k * a.lda + m : (long long)m * a.lda + k) * ES);
@@ -649,15 +792,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
   char* C = static_cast<char*>(a.C);
   const char* aux = static_cast<const char*>(a.aux);
   const bool vec_c = (a.ldc % 8 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) && n0 + cc + 8 <= a.N;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int m = m0 + rr + r;
-    if (m >= a.M) continue;
+  for (int rq = 0; rq < kSkinnyRows * 2 / 16; ++rq) {
+    const int r = rq & 1, lr = rr + r + 16 * (rq >> 1);
+    const int m = m0 + lr;
+    if (m >= a.M) break;
     float acc[8], v[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float t = 0.f;
-      for (int k = 0; k < a.K; ++k) t = fmaf(sa[rr + r][k], sb[cc + c][k], t);
+      for (int k = 0; k < a.K; ++k) t = fmaf(sa[lr][k], sb[cc + c][k], t);
       acc[c] = t;
       v[c] = a.alpha * t + bias[c];
     }
@@ -698,18 +841,28 @@ __global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
 }
 
 // out[n] (+)= sum_m X[m*ld + n]: bias gradients.  64 columns x 4 row groups per block,
-// 1024 rows per block; partial sums of several row blocks meet in f32 atomics.
+// kColsumRows rows per block (enough blocks to cover the chip for skinny N), four
+// independent loads in flight per thread; row blocks meet in f32 atomics.
+constexpr int kColsumRows = 256;
 template <int DT>
 __global__ __launch_bounds__(256) void colsum_kernel(const void* X, long long ld, int M, int N, float* out) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + c;
-  const int r0 = blockIdx.y * 1024;
-  const int r1 = min(M, r0 + 1024);
+  const int r0 = blockIdx.y * kColsumRows;
+  const int r1 = min(M, r0 + kColsumRows);
   float s = 0.f;
   if (n < N) {
     const char* base = static_cast<const char*>(X);
-    for (int m = r0 + g; m < r1; m += 4) s += load_elem<DT>(base + (static_cast<long long>(m) * ld + n) * Ty<DT>::ES);
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
+    int m = r0 + g;
+    for (; m + 12 < r1; m += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        p[u] += load_elem<DT>(base + (static_cast<long long>(m + 4 * u) * ld + n) * Ty<DT>::ES);
+    }
+    for (; m < r1; m += 4) p[0] += load_elem<DT>(base + (static_cast<long long>(m) * ld + n) * Ty<DT>::ES);
+    s = (p[0] + p[1]) + (p[2] + p[3]);
   }
   red[g][c] = s;
   __syncthreads();
@@ -721,25 +874,36 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* X, long long ld
 }
 
 // bf16 column sums with 16-byte loads: a thread owns 8 adjacent columns, 32 threads
-// span 256 columns, 8 row groups x 128 rows per block (rows 16-byte aligned, N % 8 == 0)
+// span 256 columns, 8 row groups x 32 rows per block (rows 16-byte aligned, N % 8 == 0).
+// 256-row blocks: an [8192 x 4096] gradient is 512 blocks (two per CU) instead of
+// 128, and each thread keeps its 4 row loads in flight before adding.
+constexpr int kColsumX8Rows = 256;
 __global__ __launch_bounds__(256) void colsum_bf16x8_kernel(const void* X, long long ld, int M, int N, float* out) {
   __shared__ float red[8][256];
   const int cc = threadIdx.x & 31, g = threadIdx.x >> 5;
   const int n0 = blockIdx.x * 256 + cc * 8;
-  const int r0 = blockIdx.y * 1024;
-  const int r1 = min(M, r0 + 1024);
+  const int r0 = blockIdx.y * kColsumX8Rows;
+  const int r1 = min(M, r0 + kColsumX8Rows);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto add = [&](const uint4& v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s[2 * e] += __uint_as_float(w[e] << 16);
+      s[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+    }
+  };
   if (n0 < N) {
     const uint16_t* base = static_cast<const uint16_t*>(X) + n0;
-    for (int m = r0 + g; m < r1; m += 8) {
-      const uint4 v = *reinterpret_cast<const uint4*>(base + static_cast<long long>(m) * ld);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    int m = r0 + g;
+    for (; m + 24 < r1; m += 32) {
+      uint4 v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s[2 * e] += __uint_as_float(w[e] << 16);
-        s[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
-      }
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(base + static_cast<long long>(m + 8 * u) * ld);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u]);
     }
+    for (; m < r1; m += 8) add(*reinterpret_cast<const uint4*>(base + static_cast<long long>(m) * ld));
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[g][cc * 8 + e] = s[e];
@@ -785,7 +949,7 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   }
   // K <= 16 (an MLP's first layer / last layer's input gradient): output-bandwidth kernel
   if (a.K <= 16 && a.splitk == 1) {
-    const dim3 gs((a.N + 255) / 256, (a.M + 15) / 16), bs(256);
+    const dim3 gs((a.N + 255) / 256, (a.M + gemm::kSkinnyRows - 1) / gemm::kSkinnyRows), bs(256);
     const int k3 = (a.dtype == DTP_DT_BF16 ? 4 : 0) | (a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0);
     switch (k3) {
       case 0: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, false, false>), gs, bs, 0, s, a); break;
@@ -807,11 +971,12 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   const bool fast_shape = a.dtype == DTP_DT_BF16 && a.splitk == 1 && a.K % 64 == 0 && a.vec_a && a.vec_b &&
                           (!a.trans_a || a.M % 8 == 0) && (!a.trans_b || a.N % 8 == 0) && !a.force_big;
   if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
-    const int var = a.fast >= 2 ? (a.fast - 2) & 3 : gemm::kFastDefaultVar;
+    const int var = a.fast >= 2 ? (a.fast - 2) & 7 : gemm::kFastDefaultVar;
     switch (var) {
       case 0: return gemm::launch_fast<0>(a, s);
       case 1: return gemm::launch_fast<1>(a, s);
       case 2: return gemm::launch_fast<2>(a, s);
+      case 6: return gemm::launch_fast<6>(a, s);  // var 2 with the direct per-element epilogue (A/B)
       default: return gemm::launch_fast<3>(a, s);
     }
   }
@@ -854,11 +1019,11 @@ extern "C" int dtp_colsum(const void* X, long long ld, int M, int N, int dtype, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
   if (dtype == DTP_DT_BF16 && N % 8 == 0 && ld % 8 == 0 && aligned16(X)) {
-    hipLaunchKernelGGL(gemm::colsum_bf16x8_kernel, dim3((N + 255) / 256, (M + 1023) / 1024), dim3(256), 0, s, X, ld,
-                       M, N, out);
+    hipLaunchKernelGGL(gemm::colsum_bf16x8_kernel, dim3((N + 255) / 256, (M + gemm::kColsumX8Rows - 1) / gemm::kColsumX8Rows),
+                       dim3(256), 0, s, X, ld, M, N, out);
     return check_launch("dtp_colsum(bf16x8)");
   }
-  const dim3 grid((N + 63) / 64, (M + 1023) / 1024), block(256);
+  const dim3 grid((N + 63) / 64, (M + gemm::kColsumRows - 1) / gemm::kColsumRows), block(256);
   if (dtype == DTP_DT_BF16)
     hipLaunchKernelGGL((gemm::colsum_kernel<DTP_DT_BF16>), grid, block, 0, s, X, ld, M, N, out);
   else

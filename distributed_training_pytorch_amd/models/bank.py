@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.gemm import mark_fused_grad
 from .toy import ToyModel
 
 
@@ -40,6 +41,7 @@ class ModelBank(nn.Module):
                 k = p.numel()
                 p.data = flat[i, o:o + k].view_as(p)
                 p.grad = grad[i, o:o + k].view_as(p)
+                mark_fused_grad(p)
                 o += k
             m._flat = flat[i]
         self.flat = flat

@@ -127,6 +127,37 @@ def colsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = 
     return out
 
 
+def mark_fused_grad(p: torch.Tensor, on: bool = True) -> None:
+    """Let the GEMM backward accumulate this parameter's gradient straight into
+    ``p.grad`` (the dW GEMM's epilogue adds into it; the bias column sum likewise)
+    instead of returning a fresh tensor that autograd then adds in a separate
+    kernel.  For parameters whose ``.grad`` is a persistent view of a flat gradient
+    buffer (``ModelBank``, ``FlatDDP``).  Because autograd never sees such a
+    gradient, its post-accumulate hooks do not run; hooks registered with
+    ``add_grad_ready_hook`` run instead, once the in-place write is enqueued."""
+    p._dtp_fused_grad = on
+
+
+def add_grad_ready_hook(p: torch.Tensor, fn) -> None:
+    hooks = getattr(p, "_dtp_grad_ready_hooks", None)
+    if hooks is None:
+        hooks = p._dtp_grad_ready_hooks = []
+    hooks.append(fn)
+
+
+def _fused_grad_target(p: torch.Tensor) -> torch.Tensor | None:
+    g = p.grad
+    if (getattr(p, "_dtp_fused_grad", False) and g is not None and g.dtype == torch.float32
+            and g.shape == p.shape and g.is_contiguous() and g.device == p.device):
+        return g
+    return None
+
+
+def _grad_ready(p: torch.Tensor) -> None:
+    for fn in getattr(p, "_dtp_grad_ready_hooks", ()):
+        fn(p)
+
+
 class MLPFunction(torch.autograd.Function):
     """y = L_{n-1}(... LeakyReLU(L_0(x)) ...) with every matmul on the MFMA GEMM.
 
@@ -149,6 +180,8 @@ class MLPFunction(torch.autograd.Function):
             if not last:
                 hs.append(h)
         ctx.save_for_backward(*hs, *ws)
+        # leaf parameters (not saved tensors): the backward may accumulate into their .grad
+        ctx.params = [q if q.is_leaf else None for q in params]
         ctx.L, ctx.slope, ctx.x_dtype = L, slope, x.dtype
         ctx.x_needs = ctx.needs_input_grad[0]
         return h
@@ -163,9 +196,22 @@ class MLPFunction(torch.autograd.Function):
         gW: list[torch.Tensor | None] = [None] * L
         gb: list[torch.Tensor | None] = [None] * L
         dx = None
+        need = ctx.needs_input_grad[3:]
         for l in range(L - 1, -1, -1):
-            gW[l] = gemm(dz, hs[l], trans_a=True, trans_b=True, out_dtype=torch.float32)
-            gb[l] = colsum(dz)
+            pw, pb = ctx.params[2 * l], ctx.params[2 * l + 1]
+            tw = _fused_grad_target(pw) if (pw is not None and need[2 * l]) else None
+            tb = _fused_grad_target(pb) if (pb is not None and need[2 * l + 1]) else None
+            if tw is not None:  # dW += dz^T h in the GEMM epilogue (no separate add kernel)
+                gemm(dz, hs[l], trans_a=True, trans_b=True, out=tw, accumulate=True)
+            else:
+                gW[l] = gemm(dz, hs[l], trans_a=True, trans_b=True, out_dtype=torch.float32)
+            if tb is not None:
+                colsum(dz, out=tb, accumulate=True)
+            else:
+                gb[l] = colsum(dz)
+            for q, t in ((pw, tw), (pb, tb)):
+                if t is not None:
+                    _grad_ready(q)
             if l > 0:
                 dz = gemm(dz, ws[l], trans_b=True, aux=hs[l], slope=slope, out_dtype=cd)
             elif ctx.x_needs:

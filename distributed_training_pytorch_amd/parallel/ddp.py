@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops.gemm import add_grad_ready_hook, mark_fused_grad
 from . import comm_util
 
 
@@ -79,6 +80,7 @@ class FlatDDP(nn.Module):
         self._callback_queued = False
         for p in params:
             p.register_post_accumulate_grad_hook(self._hook)
+            add_grad_ready_hook(p, self._hook)  # grads the GEMM backward accumulates in place
         if broadcast and self.world > 1:
             comm_util.broadcast_(self.flat_params, 0, group)
         self.comm = "rccl"
@@ -143,6 +145,7 @@ class FlatDDP(nn.Module):
             flat[o:o + k].copy_(p.data.reshape(-1))
             p.data = flat[o:o + k].view_as(p)
             p.grad = grad[o:o + k].view_as(p)
+            mark_fused_grad(p)
             o += k
         return flat, grad
 

@@ -96,3 +96,32 @@ def test_flatddp_bucket_views_cover_the_buffer():
     res = run_ranks(_flatddp_bucket_views, 2)
     sizes, total = res[0]
     assert len(sizes) > 2 and all(s > 0 for s in sizes) and sum(sizes) == total == 742
+
+
+def _flatddp_wide(rank, world):
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from distributed_training_pytorch_amd.models.wide import WideMLP
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(0)
+    m = WideMLP((2, 24, 24, 1))
+    ref = WideMLP((2, 24, 24, 1))
+    ref.load_state_dict(m.state_dict())
+    ddp = FlatDDP(m, first_bucket_mb=0.0005, bucket_cap_mb=0.001)
+    refd = DDP(ref.layers)
+    g = torch.Generator().manual_seed(rank)
+    x, y = torch.randn(32, 2, generator=g), torch.randn(32, 1, generator=g)
+    ddp.zero_grad()
+    torch.nn.functional.mse_loss(ddp(x), y).backward()  # GEMM backward: grads accumulated in place
+    torch.nn.functional.mse_loss(refd(x), y).backward()
+    return ddp.flat_grad.clone(), torch.cat([p.grad.reshape(-1) for p in ref.parameters()]), len(ddp._buckets)
+
+
+def test_flatddp_in_place_gemm_grads_match_torch_ddp():
+    res = run_ranks(_flatddp_wide, 2)
+    for r in range(2):
+        g, gref, nb = res[r]
+        assert nb > 1
+        torch.testing.assert_close(g, gref, rtol=1e-5, atol=1e-6)
+    assert torch.equal(res[0][0], res[1][0])

@@ -39,3 +39,34 @@ def test_wide_mlp_matches_autograd_cpu():
         torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
     assert m.flat_params.numel() == sum(p.numel() for p in m.parameters())
     torch.testing.assert_close(colsum(torch.ones(4, 3)), torch.full((3,), 4.0))
+
+
+def test_wide_mlp_fused_grad_accumulates_in_place():
+    """Parameters marked with ``mark_fused_grad`` get dz^T h added straight into
+    their (flat-view) .grad by the backward; autograd returns nothing for them, the
+    grad-ready hooks fire once per parameter per backward, and two backwards
+    accumulate exactly like AccumulateGrad."""
+    from distributed_training_pytorch_amd.ops.gemm import add_grad_ready_hook, mark_fused_grad
+
+    torch.manual_seed(0)
+    m = WideMLP((2, 16, 12, 1))
+    ps = list(m.parameters())
+    flat_grad = torch.zeros(sum(p.numel() for p in ps))
+    o, fired = 0, []
+    for p in ps:
+        p.grad = flat_grad[o:o + p.numel()].view_as(p)
+        o += p.numel()
+        mark_fused_grad(p)
+        add_grad_ready_hook(p, lambda q: fired.append(q))
+    x, y = torch.randn(33, 2), torch.randn(33, 1)
+    for _ in range(2):
+        torch.nn.functional.mse_loss(m(x), y).backward()
+    assert len(fired) == 2 * len(ps) and all(any(q is p for q in fired) for p in ps)
+    assert all(p.grad.data_ptr() == flat_grad[0:1].data_ptr() + 4 * sum(q.numel() for q in ps[:i])
+               for i, p in enumerate(ps)), "grads must stay views of the flat buffer"
+    got = flat_grad.clone()
+    ref = WideMLP((2, 16, 12, 1))
+    ref.load_state_dict(m.state_dict())
+    for _ in range(2):
+        torch.nn.functional.mse_loss(ref.reference_forward(x), y).backward()
+    torch.testing.assert_close(got, torch.cat([p.grad.reshape(-1) for p in ref.parameters()]), rtol=1e-5, atol=1e-6)

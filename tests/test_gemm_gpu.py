@@ -64,7 +64,7 @@ def test_gemm_bf16_big_tile_kernel(ta, tb):
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192)])
-@pytest.mark.parametrize("kernel", [True, 2, 3])  # default schedule, variants 0 and 1 (fast = 2 + variant)
+@pytest.mark.parametrize("kernel", [True, 2, 3, 8])  # default, variants 0, 1, 6 (direct epilogue; fast = 2 + variant)
 def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     """The LDS-DMA 256x256 kernel (row images + transposing LDS reads): every layout,
     ragged M/N edges, bias / LeakyReLU' (aux) epilogues, f32 and bf16 outputs."""
@@ -79,6 +79,33 @@ def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     aux = torch.randn(M, N, device=DEV).to(torch.bfloat16)
     cb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, aux=aux, slope=0.1, fast=kernel)
     torch.testing.assert_close(cb.float(), ref * torch.where(aux.float() > 0, 1.0, 0.1), rtol=1e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("kernel", [True, 8])  # LDS-staged vector epilogue (default) and the direct one
+def test_gemm_bf16_fast_kernel_accumulate_epilogues(ta, tb, kernel):
+    """Epilogue operands of the LDS-DMA kernel: accumulate into f32 (the in-place weight
+    gradient) and bf16 outputs, alpha + bias + LeakyReLU, and an output view whose rows
+    are not 16-byte aligned (per-element path) next to the vector path."""
+    M, N, K = 1000, 1032, 192
+    a, b = _ops(M, N, K, ta, tb, torch.bfloat16, 13)
+    ref = _ref(a, b, ta, tb)
+    bias = torch.randn(N, device=DEV)
+    old = torch.randn(M, N, device=DEV)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, out=old.clone(), accumulate=True, fast=kernel)
+    torch.testing.assert_close(c, ref + old, rtol=1e-4, atol=2e-3 * K ** 0.5)
+    oldb = old.to(torch.bfloat16)
+    cb = gemm(a, b, trans_a=ta, trans_b=tb, out=oldb.clone(), accumulate=True, fast=kernel)
+    torch.testing.assert_close(cb.float(), ref + oldb.float(), rtol=1e-2, atol=1e-1)
+    ca = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, bias=bias, act=True, slope=0.1, alpha=0.5,
+              fast=kernel)
+    torch.testing.assert_close(ca.float(), torch.nn.functional.leaky_relu(0.5 * ref + bias, 0.1), rtol=1e-2, atol=5e-2)
+    wide = torch.zeros(M, N + 3, device=DEV)
+    view = wide[:, 3:]  # ld N + 3: rows not 16-byte aligned
+    gemm(a, b, trans_a=ta, trans_b=tb, out=view, bias=bias, fast=kernel)
+    torch.testing.assert_close(view, ref + bias, rtol=1e-4, atol=2e-3 * K ** 0.5)
+    assert (wide[:, :3] == 0).all()
 
 
 @pytest.mark.parametrize("ta", [False, True])
@@ -138,7 +165,7 @@ def test_gemm_strided_views():
     torch.testing.assert_close(gemm(a2, b), _ref(a2, b, False, False), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("M", [5, 1000, 3000])
+@pytest.mark.parametrize("M", [5, 1000, 3000, 8195])
 def test_colsum(M):
     x = torch.randn(M, 77, device=DEV)
     torch.testing.assert_close(colsum(x), x.sum(0), rtol=1e-5, atol=1e-4)
