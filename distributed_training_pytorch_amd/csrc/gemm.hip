@@ -699,6 +699,9 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   constexpr bool kStaticPrio = VAR & 1, kSplitDma = VAR & 2;
+  // diagnostics only (wrong results; gemm_variants.py timing): bit 3 = no DMA after the
+  // first tile (MFMA + LDS reads alone), bit 4 = no MFMA (DMA + barriers alone)
+  constexpr bool kNoDma = VAR & 8, kNoMfma = VAR & 16;
   if constexpr (kStaticPrio) {
     if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   }
@@ -708,7 +711,7 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const bool more = kt + 1 < nk;
-    if (more) {
+    if (more && !kNoDma) {
       if constexpr (kSplitDma) stage(buf ^ 1, kt + 1, 0, 2);
       else stage(buf ^ 1, kt + 1, 0, 4);
     }
@@ -721,14 +724,16 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
       for (int j = 0; j < 4; ++j) fb[j] = fast_frag<TB>(ib, offB, j, ks);
 #pragma unroll
       for (int i = 0; i < 8; ++i) fa[i] = fast_frag<TA>(ia, offA, i, ks);
-      if constexpr (kSplitDma) {
+      if constexpr (kSplitDma && !kNoDma) {
         if (ks == 1 && more) stage(buf ^ 1, kt + 1, 2, 4);
       }
       if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(1);
+      if constexpr (!kNoMfma) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
       if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -971,12 +976,14 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   const bool fast_shape = a.dtype == DTP_DT_BF16 && a.splitk == 1 && a.K % 64 == 0 && a.vec_a && a.vec_b &&
                           (!a.trans_a || a.M % 8 == 0) && (!a.trans_b || a.N % 8 == 0) && !a.force_big;
   if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
-    const int var = a.fast >= 2 ? (a.fast - 2) & 7 : gemm::kFastDefaultVar;
+    const int var = a.fast >= 2 ? (a.fast - 2) & 31 : gemm::kFastDefaultVar;
     switch (var) {
       case 0: return gemm::launch_fast<0>(a, s);
       case 1: return gemm::launch_fast<1>(a, s);
       case 2: return gemm::launch_fast<2>(a, s);
       case 6: return gemm::launch_fast<6>(a, s);  // var 2 with the direct per-element epilogue (A/B)
+      case 10: return gemm::launch_fast<10>(a, s);  // diagnostics: var 2 without DMA
+      case 18: return gemm::launch_fast<18>(a, s);  // diagnostics: var 2 without MFMA
       default: return gemm::launch_fast<3>(a, s);
     }
   }
