@@ -544,8 +544,9 @@ DTP_DEV void bf16x8_to_f32(const uint4& g, float (&x)[8]) {
 
 // one pass = fragment rows 4H .. 4H+3 (H a template parameter: acc is indexed
 // statically, so it stays in registers)
-template <int H>
-DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], float* buf, const float (&bias)[8],
+// (J0: first of the 4 fragment columns staged, for waves holding more than 4)
+template <int H, int J0 = 0, int NJ = 4>
+DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ], float* buf, const float (&bias)[8],
                                 int m0, int wr, int ncol, bool vec, int lane) {
   const int lr = lane & 15, lg = lane >> 4, c8 = lane & 7, rl = lane >> 3;
   char* C = static_cast<char*>(a.C);
@@ -558,7 +559,7 @@ DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], 
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) buf[(16 * ii + 4 * lg + r) * kEpiStride + 16 * j + lr] = acc[4 * h + ii][j][r];
+        for (int r = 0; r < 4; ++r) buf[(16 * ii + 4 * lg + r) * kEpiStride + 16 * j + lr] = acc[4 * h + ii][J0 + j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's stores land before its own reads (LDS is in order per wave)
 #pragma unroll
     for (int t0 = 0; t0 < 8; t0 += 4) {
@@ -742,6 +743,137 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
 
   if constexpr (VAR & 4) fast_epilogue(a, acc, m0, n0, wr, wc, lr, lg);  // direct per-element stores (A/B)
   else fast_epilogue_lds(a, acc, lds, m0, n0, wave, wr, wc, lane);
+}
+
+// ---------------------------------------------------------------------------
+// One-wave-per-SIMD variant: 4 waves (2 x 2), each a 128x128 sub-tile (64
+// accumulators of 16x16x32 MFMAs = 256 registers: the unified VGPR/AGPR file at one
+// wave per SIMD).  The same LDS-DMA images, swizzles and fragment reads as above,
+// but the wave pipelines its own LDS reads instead of relying on a second wave:
+//   k-step 1's 16 fragment reads are in flight during k-step 0's 64 MFMAs; the
+//   per-tile barrier sits between the two k-steps, and right after it the NEXT
+//   tile's k-step-0 reads are issued, so they land during k-step 1's MFMAs.
+//   The DMA of tile t+2 goes out right after that barrier (its buffer was just
+//   released), one whole tile ahead of its use.
+// ---------------------------------------------------------------------------
+constexpr int kW4Threads = 256;
+
+template <bool TRANS>
+DTP_DEV void w4_sources(const char* (&src)[8], const char* base, long long ld, int r0, int R, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = 4 * i + wave;  // the 1-KiB chunk of the image this instruction fills
+    if constexpr (!TRANS) {
+      const int row = q * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ fswz(row);
+      const int rr = min(r0 + row, R - 1);
+      src[i] = base + (static_cast<long long>(rr) * ld + c * 8) * 2;
+    } else {
+      const int k = q * 2 + (lane >> 5);
+      const int c = (lane & 31) ^ (fswz(k) << 1);
+      const int col = min(r0 + c * 8, R - 8);
+      src[i] = base + (static_cast<long long>(k) * ld + col) * 2;
+    }
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(DtpGemmArgs a) {
+  constexpr int BK = 64;
+  __shared__ __align__(16) char lds[2 * 2 * kFastImg];  // 128 KiB; epilogue: 4 x 17 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const TileId id = decode_tile<256, 256>(a);
+  const int m0 = id.m0, n0 = id.n0, nk = a.K / BK;
+
+  const char* srcA[8];
+  const char* srcB[8];
+  w4_sources<TA>(srcA, static_cast<const char*>(a.A), a.lda, m0, a.M, wave, lane);
+  w4_sources<TB>(srcB, static_cast<const char*>(a.B), a.ldb, n0, a.N, wave, lane);
+  const long long kbA = TA ? static_cast<long long>(BK) * a.lda * 2 : BK * 2;
+  const long long kbB = TB ? static_cast<long long>(BK) * a.ldb * 2 : BK * 2;
+  auto stage = [&](int buf, int kt) {
+    char* img = lds + buf * 2 * kFastImg;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcA[i] + kt * kbA), (lds_void_t*)(img + (4 * i + wave) * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[i] + kt * kbB),
+                                       (lds_void_t*)(img + kFastImg + (4 * i + wave) * 1024), 16, 0, 0);
+    }
+  };
+  int offA[TA ? 8 : 2], offB[TB ? 8 : 2];
+  fast_offsets<TA, 8>(offA, wr * 128, lane);
+  fast_offsets<TB, 8>(offB, wc * 128, lane);
+  auto frags = [&](int buf, int ks, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    const char* ia = lds + buf * 2 * kFastImg;
+    const char* ib = ia + kFastImg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[j] = fast_frag<TB>(ib, offB, j, ks);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = fast_frag<TA>(ia, offA, i, ks);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed, tile 1 may still fly
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  frags(0, 0, fa0, fb0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    frags(buf, 1, fa1, fb1);  // k-step 1 reads fly during k-step 0's MFMAs
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+    // every read of `buf` has returned and tile kt+1's DMA (issued one tile ago) has landed
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 2 < nk) stage(buf, kt + 2);
+    if (kt + 1 < nk) frags(buf ^ 1, 0, fa0, fb0);  // next tile's k-step 0 flies during k-step 1's MFMAs
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the operand images: they become epilogue staging
+
+  float* ebuf = reinterpret_cast<float*>(lds) + wave * kEpiWaveFloats;
+  const uintptr_t cp = reinterpret_cast<uintptr_t>(a.C), ap = reinterpret_cast<uintptr_t>(a.aux);
+  const bool aligned = a.ldc % 8 == 0 && (cp & 15) == 0 && (!a.aux || (a.ldaux % 8 == 0 && (ap & 15) == 0));
+  auto half = [&](auto JH) {
+    constexpr int jh = decltype(JH)::value;
+    const int ncol = n0 + wc * 128 + 64 * jh + 8 * (lane & 7);
+    const bool vec = aligned && ncol + 8 <= a.N;
+    float bias[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bias[c] = (a.bias && ncol + c < a.N) ? a.bias[ncol + c] : 0.f;
+    fast_epilogue_pass<0, 4 * jh, 8>(a, acc, ebuf, bias, m0, wr, ncol, vec, lane);
+    fast_epilogue_pass<1, 4 * jh, 8>(a, acc, ebuf, bias, m0, wr, ncol, vec, lane);
+  };
+  half(std::integral_constant<int, 0>{});
+  half(std::integral_constant<int, 1>{});
+}
+
+int launch_w4(const DtpGemmArgs& a, hipStream_t s) {
+  const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const dim3 gf((unsigned)tiles), bf(kW4Threads);
+  switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
+    case 0: hipLaunchKernelGGL((gemm_w4_kernel<false, false>), gf, bf, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((gemm_w4_kernel<false, true>), gf, bf, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_w4_kernel<true, false>), gf, bf, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_w4_kernel<true, true>), gf, bf, 0, s, a); break;
+  }
+  return check_launch("dtp_gemm(LDS-DMA 256x256, 4 waves)");
 }
 
 constexpr int kFastDefaultVar = 2;  // next tile's DMA split over the k-steps: +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl; the ring schedules
@@ -982,6 +1114,7 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
       case 1: return gemm::launch_fast<1>(a, s);
       case 2: return gemm::launch_fast<2>(a, s);
       case 6: return gemm::launch_fast<6>(a, s);  // var 2 with the direct per-element epilogue (A/B)
+      case 7: return gemm::launch_w4(a, s);  // one wave per SIMD, 128x128 per wave
       case 10: return gemm::launch_fast<10>(a, s);  // diagnostics: var 2 without DMA
       case 18: return gemm::launch_fast<18>(a, s);  // diagnostics: var 2 without MFMA
       default: return gemm::launch_fast<3>(a, s);
