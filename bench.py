@@ -97,7 +97,8 @@ def main():
         runner = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
         per_rank_batch = geom.batch_size_at(0)
         train = runner.train
-        sync = runner.synchronize
+        # the xGMI timeout word is checked right after the timed region (check_comm below)
+        sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm}
 
     # warmup (untimed)
@@ -117,6 +118,7 @@ def main():
 
     final_loss = None
     if a.impl == "native":
+        runner.check_comm()  # raises if any in-kernel exchange of the run timed out
         final_loss = runner.losses(runner.t - 1, runner.t)[0].tolist()
         runner.close()
     else:

@@ -168,6 +168,9 @@ def _declare(lib):
         "dtp_mlp_workspace_floats": (c_int, [c_int] * 4),
         "dtp_mlp_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
+        "dtp_train_engine_create": (c_void_p, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
+        "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_void_p]),
+        "dtp_train_engine_destroy": (None, [c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
@@ -270,6 +273,11 @@ def check(rc: int, what: str):
 def stream_ptr(stream: torch.cuda.Stream | None = None) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)
+
+
+def raw_stream(device_index: int) -> int:
+    """The current stream of a device as a raw hipStream_t (no Stream object built)."""
+    return torch._C._cuda_getCurrentRawStream(device_index)
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

@@ -90,13 +90,29 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   const int ydim = ce ? 1 : S::OUT;
   const float slope = a.hp.slope;
 
-  // ---- setup: workspace (zero pads, then scatter), dataset -> LDS, owned params
+  // ---- setup. Every global read of the prologue (owned params and moments, step
+  // and exchange counters, the dataset) is issued before the first wait, so a
+  // launch pays ONE memory round trip before its first step, not three.
   float* __restrict__ gp = a.params + (size_t)model * P;
   float* __restrict__ ws = a.wsp + (size_t)model * SC::WS;
-  for (int e = tid; e < SC::WS; e += kBlock) ws[e] = 0.f;
-  for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   const SamplerCfg smp = a.smp;
   const bool cached = a.cache_data && smp.n * (S::IN + ydim) <= kDataCache;
+  int pf[NPT], pb[NPT], tp[NPT], pfl[NPT];
+  float pw[NPT], mr[NPT], vr[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = tid + k * kBlock;
+    scal_pos<S>(p < P ? p : 0, pf[k], pb[k], tp[k], pfl[k]);
+    const bool own = p < P;
+    pw[k] = own ? gp[p] : 0.f;
+    mr[k] = (kUpdate && own) ? a.opt_m[(size_t)model * P + p] : 0.f;
+    vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
+  }
+  const int t0 = a.step[model];
+  unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
+  if constexpr (kScalarFwd)
+    for (int e = tid; e < SC::WS; e += kBlock) ws[e] = 0.f;
+  for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   if (cached) {
     for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
     for (int e = tid; e < smp.n * ydim; e += kBlock) sm.data[smp.n * S::IN + e] = a.Y[e];
@@ -104,30 +120,17 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   const float* __restrict__ Xg = a.X;
   const float* __restrict__ Yg = a.Y;
   const int yoff = smp.n * S::IN;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int pf[NPT], pb[NPT], tp[NPT], pfl[NPT];
-  float pw[NPT], mr[NPT], vr[NPT];
+  if constexpr (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pad zeros before the scatter
+  __syncthreads();  // weight blocks zeroed (pads stay 0) before the owners scatter into them
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int p = tid + k * kBlock;
-    scal_pos<S>(p < P ? p : 0, pf[k], pb[k], tp[k], pfl[k]);
-    pw[k] = 0.f;
-    mr[k] = 0.f;
-    vr[k] = 0.f;
-    if (p < P) {
-      pw[k] = gp[p];
+    if (tid + k * kBlock < P) {
       if (kScalarFwd) ws[pf[k]] = pw[k];
       sm.wb[pfl[k]] = pw[k];
       if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
-      if (kUpdate) {
-        mr[k] = a.opt_m[(size_t)model * P + p];
-        if (kAdam) vr[k] = a.opt_v[(size_t)model * P + p];
-      }
     }
   }
   // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
-  const int t0 = a.step[model];
   const bool explicit_idx = smp.mode == SAMPLER_EXPLICIT;
   int epoch = explicit_idx ? 0 : t0 / smp.steps_per_epoch;
   int bi = explicit_idx ? 0 : t0 - epoch * smp.steps_per_epoch;
@@ -175,10 +178,9 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
     }
   };
   if (kAdam) fill_adam(0);
-  unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
   float* const stg_pack = &sm.stage[wave][0][0];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // workspace weights in L2
+  __syncthreads();  // scattered weight blocks and the Adam table visible to every wave
 
   for (int it = 0; it < a.n_steps; ++it) {
     DTP_STAMP(0);
@@ -418,31 +420,63 @@ using dtp::set_err;
   X(2, 10, 5, 4)            \
   X(2, 15, 5, 1)
 
-template <class S>
-int launch_train(const DtpTrainArgs* a, int mode, hipStream_t st) {
-  dim3 grid(a->n_models), block(dtp::kBlock);
-  switch (mode) {
-    case DTP_MODE_GRAD:
-      if (a->n_steps != 1) return set_err(-4, "MODE_GRAD requires n_steps == 1");
-      hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_GRAD>), grid, block, 0, st, *a);
-      break;
-    case DTP_MODE_ADAM:
-      hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_ADAM>), grid, block, 0, st, *a);
-      break;
-    case DTP_MODE_SGD:
-      hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_SGD>), grid, block, 0, st, *a);
-      break;
-    case DTP_MODE_XGMI_ADAM:
-      hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_XGMI_ADAM>), grid, block, 0, st, *a);
-      break;
-    case DTP_MODE_XGMI_SGD:
-      hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_XGMI_SGD>), grid, block, 0, st, *a);
-      break;
-    default:
-      return set_err(-2, "unknown train mode");
-  }
-  return check_launch("mlp_train_kernel");
+using TrainLaunchFn = void (*)(const DtpTrainArgs&, hipStream_t);
+
+template <class S, int MODE>
+void launch_mode(const DtpTrainArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((dtp::mlp_train_kernel<S, MODE>), dim3(a.n_models), dim3(dtp::kBlock), 0, st, a);
 }
+
+// the kernel instance of (shape S, mode), resolved once (the native engine keeps it)
+template <class S>
+TrainLaunchFn train_fn(int mode) {
+  switch (mode) {
+    case DTP_MODE_GRAD: return &launch_mode<S, DTP_MODE_GRAD>;
+    case DTP_MODE_ADAM: return &launch_mode<S, DTP_MODE_ADAM>;
+    case DTP_MODE_SGD: return &launch_mode<S, DTP_MODE_SGD>;
+    case DTP_MODE_XGMI_ADAM: return &launch_mode<S, DTP_MODE_XGMI_ADAM>;
+    case DTP_MODE_XGMI_SGD: return &launch_mode<S, DTP_MODE_XGMI_SGD>;
+    default: return nullptr;
+  }
+}
+
+TrainLaunchFn resolve_train(int in, int h, int nl, int out, int mode) {
+#define X(I, H, N, O) \
+  if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false>>(mode);
+  DTP_TRAIN_SHAPES(X)
+#undef X
+  return nullptr;
+}
+
+int validate_train(const DtpTrainArgs* a, int mode) {
+  if (!a) return set_err(-1, "null args");
+  if (a->n_models <= 0 || a->n_steps <= 0) return set_err(-1, "n_models and n_steps must be positive");
+  if (a->smp.batch <= 0 || a->smp.n <= 0) return set_err(-1, "empty dataset or batch");
+  if (a->smp.mode != dtp::SAMPLER_EXPLICIT && (a->smp.steps_per_epoch <= 0 || a->smp.num_samples <= 0))
+    return set_err(-1, "bad sampler geometry");
+  if (a->smp.mode == dtp::SAMPLER_EXPLICIT && !a->idx) return set_err(-1, "explicit sampler without indices");
+  if (a->loss_log && a->loss_log_cap <= 0) return set_err(-1, "loss_log_cap must be positive");
+  if (!a->wsp) return set_err(-1, "the weight workspace (wsp) is required");
+  if (!a->params || !a->X || !a->Y || !a->step) return set_err(-1, "params, X, Y and step are required");
+  if (mode == DTP_MODE_GRAD && !a->grad_out) return set_err(-1, "MODE_GRAD needs grad_out");
+  if (mode != DTP_MODE_GRAD && !a->opt_m) return set_err(-1, "optimizer modes need opt_m");
+  if ((mode == DTP_MODE_ADAM || mode == DTP_MODE_XGMI_ADAM) && !a->opt_v) return set_err(-1, "Adam needs opt_v");
+  if (mode == DTP_MODE_XGMI_ADAM || mode == DTP_MODE_XGMI_SGD) {
+    if (!a->peers || !a->epoch) return set_err(-1, "xGMI modes need the peer table and epoch counters");
+    if (a->smp.world < 1 || a->smp.world > dtp::kXgmiMaxWorld || a->smp.rank < 0 || a->smp.rank >= a->smp.world)
+      return set_err(-1, "xGMI modes serve 1..8 ranks");
+  }
+  return 0;
+}
+
+// Native step executor: the argument block and the kernel instance are fixed at
+// creation, so a call costs one kernel launch (no per-call marshalling or
+// dispatch on the host; the Python side calls it with (handle, n_steps, stream)).
+struct TrainEngine {
+  DtpTrainArgs a;
+  TrainLaunchFn fn;
+  int mode;
+};
 
 template <class S>
 int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
@@ -473,20 +507,40 @@ int dtp_mlp_param_count(int in, int h, int nl, int out) {
 }
 
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream) {
-  if (!a) return set_err(-1, "null args");
-  if (a->n_models <= 0 || a->n_steps <= 0) return set_err(-1, "n_models and n_steps must be positive");
-  if (a->smp.batch <= 0 || a->smp.n <= 0) return set_err(-1, "empty dataset or batch");
-  if (a->smp.mode != dtp::SAMPLER_EXPLICIT && (a->smp.steps_per_epoch <= 0 || a->smp.num_samples <= 0))
-    return set_err(-1, "bad sampler geometry");
-  if (a->loss_log && a->loss_log_cap <= 0) return set_err(-1, "loss_log_cap must be positive");
-  if (!a->wsp) return set_err(-1, "the weight workspace (wsp) is required");
-  hipStream_t st = (hipStream_t)stream;
-#define X(I, H, N, O) \
-  if (in == I && h == H && nl == N && out == O) return launch_train<dtp::Stage<I, H, N, O, false>>(a, mode, st);
-  DTP_TRAIN_SHAPES(X)
-#undef X
-  return set_err(-2, "mlp shape not instantiated for the fused train kernel");
+  if (int rc = validate_train(a, mode)) return rc;
+  if (mode == DTP_MODE_GRAD && a->n_steps != 1) return set_err(-4, "MODE_GRAD requires n_steps == 1");
+  TrainLaunchFn fn = resolve_train(in, h, nl, out, mode);
+  if (!fn) return set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
+  fn(*a, (hipStream_t)stream);
+  return check_launch("mlp_train_kernel");
 }
+
+void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
+  if (validate_train(a, mode)) return nullptr;
+  TrainLaunchFn fn = resolve_train(in, h, nl, out, mode);
+  if (!fn) {
+    set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
+    return nullptr;
+  }
+  auto* e = new TrainEngine();
+  e->a = *a;
+  e->fn = fn;
+  e->mode = mode;
+  return e;
+}
+
+// n_steps iterations in ONE persistent launch on `stream`
+int dtp_train_engine_run(void* h, int n_steps, void* stream) {
+  auto* e = static_cast<TrainEngine*>(h);
+  if (!e) return set_err(-1, "null engine");
+  if (n_steps <= 0) return set_err(-1, "n_steps must be positive");
+  if (e->mode == DTP_MODE_GRAD && n_steps != 1) return set_err(-4, "MODE_GRAD requires n_steps == 1");
+  e->a.n_steps = n_steps;
+  e->fn(e->a, (hipStream_t)stream);
+  return check_launch("mlp_train_kernel");
+}
+
+void dtp_train_engine_destroy(void* h) { delete static_cast<TrainEngine*>(h); }
 
 // diagnostic: toy shape, Adam, phase stamps into a->status (as u64[n_models][8][16])
 int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream) {

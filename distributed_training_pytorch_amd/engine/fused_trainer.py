@@ -83,6 +83,9 @@ class FusedTrainer:
         self.t = 0  # host mirror of the step counter
         self._idx_stream = EpochIndexStream(geom)
         self._graphs: dict = {}
+        self._engine = None  # native step executor (csrc/mlp_train.hip: dtp_train_engine_*)
+        self._dev_index = self.device.index if self.device.index is not None else (
+            torch.cuda.current_device() if self.device.type == "cuda" else -1)
         self._xgmi = None
         self.comm = self._resolve_comm()
         # DDP construction semantics: every rank starts from rank 0's weights
@@ -119,8 +122,21 @@ class FusedTrainer:
             raise ValueError("comm='xgmi' is the single-node (<= 8 GPU) in-kernel exchange; use 'rccl' beyond")
         return c
 
+    def _agree(self, ok: bool) -> bool:
+        """True on every rank iff ``ok`` on every rank (one 1-element all-reduce)."""
+        if self.world == 1:
+            return ok
+        flag = torch.tensor([0.0 if ok else 1.0], device="cpu")
+        comm_util.all_reduce_(flag, self.group)
+        return flag.item() == 0.0
+
     def _setup_xgmi(self):
-        """Map the peers' exchange buffers; self-test; fall back to RCCL on any failure."""
+        """Map the peers' exchange buffers; self-test; fall back to RCCL on any failure.
+
+        Every collective here is issued by every rank whatever failed locally: the
+        ranks agree on the setup before the self-test (whose first op is a
+        collective), and again on its result, so a failure on some ranks only can
+        never leave the others in a different collective."""
         from ..parallel.xgmi import XgmiExchange
 
         ok, why = True, ""
@@ -128,15 +144,10 @@ class FusedTrainer:
             self._xgmi = XgmiExchange(self.n_models, self.spec.P, self.device, self.group)
         except Exception as e:  # IPC / peer access unavailable
             ok, why = False, f"setup: {e}"
+        ok = self._agree(ok)
         if ok and self.cfg.xgmi_selftest:
-            try:
-                ok, why = self._xgmi_selftest()
-            except Exception as e:
-                ok, why = False, f"selftest: {e}"
-        if self.world > 1:
-            flag = torch.tensor([0.0 if ok else 1.0], device="cpu")
-            comm_util.all_reduce_(flag, self.group)  # every rank must agree on the path
-            ok = flag.item() == 0.0
+            ok, why = self._xgmi_selftest()
+            ok = self._agree(ok)
         if not ok:
             if self.rank == 0:
                 print(f"[dtp] xGMI exchange unavailable ({why or 'a peer failed'}); using RCCL", flush=True)
@@ -146,43 +157,76 @@ class FusedTrainer:
                 self._xgmi.close()
                 self._xgmi = None
             self.comm = "rccl"
+            # the self-test restored every rank's state; re-broadcasting rank 0's
+            # replica anyway makes the fallback safe by construction
+            comm_util.broadcast_(self.params, 0, self.group)
+
+    def _state(self):
+        return (self.params, self.m, self.v, self.step_ctr, self.loss_log)
 
     def _xgmi_selftest(self) -> tuple[bool, str]:
-        """Two exchanges of known values through the real kernel path: one fused
-        step in MODE_XGMI on a scratch copy must reproduce the host all-reduce."""
+        """Two exchanges (both buffer parities) of one real fused step through the
+        in-kernel xGMI path must reproduce the host all-reduce path.  The training
+        state is restored on every exit, and every rank issues the same collectives
+        whatever fails locally."""
+        import os
+
         lib = nat.load()
-        saved = [t.clone() for t in (self.params, self.m, self.v, self.step_ctr, self.loss_log)]
+        saved = [t.clone() for t in self._state()]
         saved_t = self.t
-        # reference: local grads via MODE_GRAD, host all-reduce, flat optimizer
-        a = self._train_args(1, nat.MODE_GRAD, None)
-        nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
-                  "selftest grad")
-        buf = self.comm_buf.clone()
-        comm_util.all_reduce_(buf, self.group)
-        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.optim,
-                            grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world,
-                            slope=self.spec.slope)
-        ref_p = self.params.clone()
-        ref_l = self.loss_log[0].clone()
-        for t, s0 in zip((self.params, self.m, self.v, self.step_ctr, self.loss_log), saved):
-            t.copy_(s0)
-        # the same step through the in-kernel xGMI exchange (twice: both parities)
-        for _ in range(2):
-            for t, s0 in zip((self.params, self.m, self.v, self.step_ctr, self.loss_log), saved):
+
+        def restore():
+            for t, s0 in zip(self._state(), saved):
                 t.copy_(s0)
-            self._launch(1)
-            torch.cuda.synchronize(self.device)
-            st = self._xgmi.status[:2].tolist()
-            if st[0]:
-                return False, f"timeout at epoch {st[1]}"
-            err = (self.params - ref_p).abs().max().item()
-            lerr = (self.loss_log[0] - ref_l).abs().max().item()
-            if not (err <= 1e-5 and lerr <= 1e-5):
-                return False, f"mismatch vs host all-reduce (param err {err:.3e}, loss err {lerr:.3e})"
-        for t, s0 in zip((self.params, self.m, self.v, self.step_ctr, self.loss_log), saved):
-            t.copy_(s0)
-        self.t = saved_t
-        return True, ""
+
+        try:
+            ok, why = True, ""
+            # reference: local grads via MODE_GRAD, host all-reduce, flat optimizer
+            buf = torch.zeros_like(self.comm_buf)
+            try:
+                a = self._train_args(1, nat.MODE_GRAD, None)
+                nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
+                          "selftest grad")
+                buf.copy_(self.comm_buf)
+            except Exception as e:
+                ok, why = False, f"selftest grad: {e}"
+            comm_util.all_reduce_(buf, self.group)  # issued on every rank
+            ok = self._agree(ok)
+            if not ok:
+                return False, why or "a peer failed the self-test"
+            flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.optim,
+                                grad_scale=1.0 / self.world, loss_log=self.loss_log, loss_scale=1.0 / self.world,
+                                slope=self.spec.slope)
+            ref_p = self.params.clone()
+            ref_l = self.loss_log[0].clone()
+            # the same step through the in-kernel exchange, twice (both parities); every
+            # rank runs both launches (a rank that stopped early would leave its peers
+            # waiting out the timeout); in-kernel waits are bounded
+            errs = []
+            for _ in range(2):
+                restore()
+                try:
+                    self._launch(1)
+                    torch.cuda.synchronize(self.device)
+                except Exception as e:
+                    errs.append(f"launch: {e}")
+                    break
+                st = self._xgmi.status[:2].tolist()
+                if st[0]:
+                    errs.append(f"timeout at epoch {st[1]}")
+                    continue
+                err = (self.params - ref_p).abs().max().item()
+                lerr = (self.loss_log[0] - ref_l).abs().max().item()
+                if not (err <= 1e-5 and lerr <= 1e-5):
+                    errs.append(f"mismatch vs host all-reduce (param err {err:.3e}, loss err {lerr:.3e})")
+            if os.environ.get("DTP_XGMI_SELFTEST_FAIL_RANK", "") == str(self.rank):
+                errs.append("forced failure (DTP_XGMI_SELFTEST_FAIL_RANK)")  # test hook
+            return (not errs), "; ".join(errs)
+        except Exception as e:
+            return False, f"selftest: {e}"
+        finally:
+            restore()
+            self.t = saved_t
 
     def _hyper(self, grad_scale: float) -> nat.Hyper:
         return self.optim.hyper(self.spec.slope, grad_scale)
@@ -235,7 +279,7 @@ class FusedTrainer:
                 self._launch_explicit(k)
             elif self.cfg.launch == "persistent":
                 k = min(remaining, self.cfg.steps_per_launch)
-                self._launch(k)
+                self._run_engine(k)
             elif self.cfg.launch == "graph":
                 G = self.cfg.steps_per_launch
                 if remaining >= G:
@@ -246,9 +290,24 @@ class FusedTrainer:
                     self._launch(1)
             else:
                 k = 1
-                self._launch(1)
+                self._run_engine(1)
             remaining -= k
             self.t += k
+
+    def _run_engine(self, k: int):
+        """k iterations in one persistent launch through the native executor: the
+        argument block is built once, so a call is one C call + one kernel launch."""
+        e = self._engine
+        if e is None:
+            lib = nat.load()
+            mode = self._update_mode()
+            a = self._train_args(1, mode, None)
+            e = lib.dtp_train_engine_create(ctypes.byref(a), *self.spec.key[:4], mode)
+            if not e:
+                nat.check(-1, "dtp_train_engine_create")
+            self._engine = e
+            self._engine_run = lib.dtp_train_engine_run
+        nat.check(self._engine_run(e, k, nat.raw_stream(self._dev_index)), "dtp_train_engine_run")
 
     def _launch(self, k: int, idx: torch.Tensor | None = None, batch_override: int | None = None):
         lib = nat.load()
@@ -377,6 +436,12 @@ class FusedTrainer:
         if self._xgmi is not None:
             self._xgmi.check_status()
 
+    def check_comm(self):
+        """Raise if the in-kernel exchange hit its (sticky) timeout. One small read;
+        call it where the host syncs anyway (loss readback, checkpoints)."""
+        if self._xgmi is not None:
+            self._xgmi.check_status()
+
     def losses(self, t0: int, t1: int) -> torch.Tensor:
         """Global mean losses of steps [t0, t1) as a CPU tensor [t1-t0, n_models] (syncs)."""
         cap = self.loss_log.shape[0]
@@ -402,6 +467,9 @@ class FusedTrainer:
 
     def close(self):
         lib = nat.load() if self.native else None
+        if self._engine is not None and lib is not None:
+            lib.dtp_train_engine_destroy(self._engine)
+        self._engine = None
         for k, h in list(self._graphs.items()):
             if isinstance(h, int) and lib is not None:
                 lib.dtp_graph_destroy(ctypes.c_void_p(h))

@@ -157,6 +157,9 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
     if config.resume and config.checkpoint_dir:
         st = checkpoint.load(config.checkpoint_dir)
         if st is not None:
+            if st.get("engine", "fused") != "fused":
+                raise RuntimeError(f"{config.checkpoint_dir} holds a {st['engine']!r}-engine checkpoint; "
+                                   "resume it with the same engine")
             tr.load_state_dict(st)
             start = tr.t
             rank_print(rank, f"resumed from {config.checkpoint_dir} at iteration {start}")
@@ -177,6 +180,7 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
                 tr.train(n)
             with timer.phase("loss_readback"):
                 ls = tr.losses(it, it + n)  # one host sync per chunk
+                tr.check_comm()  # sticky xGMI timeout word: raise now, never train on partial sums
             for k in range(n):
                 logger.log({"loss/lossX": ls[k, 0].item()}, step=it + k, commit=False)
                 logger.log({"loss/lossY": ls[k, 1].item()}, step=it + k)
@@ -186,7 +190,8 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
         faults.check(it)
         if config.checkpoint_dir and config.checkpoint_every and it % config.checkpoint_every == 0:
             tr.synchronize()
-            checkpoint.save({**tr.state_dict(), "config": vars(config)}, config.checkpoint_dir, it)
+            checkpoint.save({**tr.state_dict(), "engine": "fused", "config": vars(config)},
+                            config.checkpoint_dir, it)
     tr.synchronize()
     dt = time.perf_counter() - t0
     if pbar is not None:
@@ -194,7 +199,7 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
     if config.check_replicas:
         check_replicas(tr.params)
     if config.checkpoint_dir:
-        checkpoint.save({**tr.state_dict(), "config": vars(config)}, config.checkpoint_dir, it)
+        checkpoint.save({**tr.state_dict(), "engine": "fused", "config": vars(config)}, config.checkpoint_dir, it)
     final = tr.losses(it - 1, it)[0].tolist() if it > 0 else [float("nan")] * 2
     samples = geom.batch * (it - start) * world
     tr.close()
@@ -221,11 +226,30 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     rank_print(rank, f"engine: module (FlatDDP over {ddp.comm})")
     opt = FlatOptimizer(bank.flat, bank.flat_grad, _optim(config))
     lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else torch.nn.MSELoss()
+    start = 0
+    if config.resume and config.checkpoint_dir:
+        st = checkpoint.load(config.checkpoint_dir)
+        if st is not None:
+            if st.get("engine") != "module":
+                raise RuntimeError(f"{config.checkpoint_dir} holds a {st.get('engine', 'fused')!r}-engine "
+                                   "checkpoint; resume it with the same engine")
+            with torch.no_grad():
+                bank.flat.copy_(st["params"].to(bank.flat.dtype))
+            opt.load_state_dict(st["optim_state"])
+            start = int(st["iteration"])
+            rank_print(rank, f"resumed from {config.checkpoint_dir} at iteration {start}")
+
+    def _save(it_done):
+        checkpoint.save({"engine": "module", "params": bank.flat.detach(), "optim_state": opt.state_dict(),
+                         "config": vars(config)}, config.checkpoint_dir, it_done)
+
     pbar = _progress(rank, config.iters, config)
+    if pbar is not None and start:
+        pbar.update(start)
     timer = PhaseTimer(device)
     t0 = time.perf_counter()
     lbuf = torch.zeros(2, device=device)
-    for it in range(config.iters):
+    for it in range(start, config.iters):
         faults.check(it)
         with timer.phase("data"):
             idx = idx_stream.indices(it) if idx_stream is not None else geom.indices(it)
@@ -250,15 +274,20 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
             logger.log({"loss/lossY": lbuf[1].item()}, step=it)
         if pbar is not None:
             pbar.update(1)
+        if config.checkpoint_dir and config.checkpoint_every and (it + 1) % config.checkpoint_every == 0:
+            _save(it + 1)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
+    ddp.check_comm()
     dt = time.perf_counter() - t0
     if pbar is not None:
         pbar.close()
     if config.check_replicas:
         check_replicas(bank.flat)
+    if config.checkpoint_dir:
+        _save(config.iters)
     return {"final_loss": lbuf.tolist(), "iters": config.iters,
-            "samples_per_s": geom.batch * config.iters * world / max(dt, 1e-9), "engine": "module",
+            "samples_per_s": geom.batch * (config.iters - start) * world / max(dt, 1e-9), "engine": "module",
             **({"phases": timer.summary()} if trace_enabled() else {})}
 
 

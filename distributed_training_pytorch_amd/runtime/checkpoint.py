@@ -34,7 +34,9 @@ def save(state: dict, directory: str | os.PathLike, step: int, keep: int = 0, ra
     d = Path(directory)
     d.mkdir(parents=True, exist_ok=True)
     payload = _to_plain(dict(state))
-    payload["step"] = int(step)
+    # the host iteration gets a key of its own: "step" belongs to the engines'
+    # per-model optimizer step counters and must survive the round trip
+    payload["iteration"] = int(step)
     payload["rng_cpu"] = torch.get_rng_state()
     tmp = d / f".last.pt.tmp.{os.getpid()}"
     torch.save(payload, tmp)

@@ -125,3 +125,24 @@ def test_flat_ddp_xgmi_matches_host_path():
         for ga, gb in zip(a[r][0], b[r][0]):
             torch.testing.assert_close(ga, gb, rtol=1e-6, atol=1e-7)
     assert all(torch.equal(x, y) for x, y in zip(a[0][0], a[1][0]))
+
+
+def _forced_selftest_failure(rank, world):
+    import os
+
+    os.environ["DTP_XGMI_SELFTEST_FAIL_RANK"] = "1"  # only rank 1 reports a failed self-test
+    return _gpu_rank(rank, world, "xgmi", STEPS, "persistent")
+
+
+def test_xgmi_selftest_failure_on_one_rank_falls_back_consistently():
+    """A self-test failure on ONE rank moves every rank to the RCCL path, with the
+    trial step undone everywhere: the replicas stay identical and equal the
+    single-process reference."""
+    res = run_ranks(_forced_selftest_failure, 2, (), timeout=300)
+    ref_p, ref_l = _reference(2, STEPS)
+    for r in range(2):
+        p, l, used = res[r]
+        assert used == "rccl", f"rank {r} kept {used}"
+        torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
+    assert torch.equal(res[0][0], res[1][0]), "replicas diverged after the fallback"
