@@ -68,6 +68,10 @@ def parse():
 
 def main():
     a = parse()
+    if torch.cuda.device_count() > 0:  # counting devices does not initialise the GPU
+        from distributed_training_pytorch_amd import _native
+
+        _native.set_wait_mode()  # DTP_WAIT_MODE; before the first GPU touch
     if a.share_gpu and torch.cuda.device_count() > 0:
         os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
     rank, world, local_rank = dist_env.init_from_env(backend="gloo" if a.share_gpu else None,

@@ -17,7 +17,8 @@ from pathlib import Path
 
 import torch  # noqa: F401  -- must be imported first: libdtp.so binds to torch's HIP runtime
 
-LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libdtp.so"
+# DTP_LIB selects an A/B build (``build.variant``); default: the in-tree library
+LIB_PATH = Path(os.environ.get("DTP_LIB") or Path(__file__).resolve().parent / "_lib" / "libdtp.so")
 
 c_int = ctypes.c_int
 c_float = ctypes.c_float
@@ -282,6 +283,29 @@ def raw_stream(device_index: int) -> int:
 
 def ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else int(t.data_ptr())
+
+
+_WAIT_FLAGS = {"auto": 0x0, "spin": 0x1, "yield": 0x2, "blocking": 0x4}  # hipDeviceSchedule*
+
+
+def set_wait_mode(mode: str | None = None) -> str:
+    """How host threads wait for GPU completion (``hipSetDeviceFlags``).
+
+    ``spin`` keeps the waiting thread polling the completion signal instead of
+    sleeping on an interrupt: a ``synchronize`` after a short launch returns a few
+    microseconds sooner, at the price of one busy CPU core per rank while it
+    waits.  Call before the process touches the GPU.  ``mode=None`` reads
+    ``DTP_WAIT_MODE`` (default ``auto``: the runtime's own policy)."""
+    mode = mode or os.environ.get("DTP_WAIT_MODE", "auto")
+    if mode not in _WAIT_FLAGS:
+        raise ValueError(f"wait mode {mode!r} not in {sorted(_WAIT_FLAGS)}")
+    if mode == "auto":
+        return mode
+    hip = ctypes.CDLL("libamdhip64.so.7")  # torch's own runtime (same soname, already loaded)
+    rc = hip.hipSetDeviceFlags(ctypes.c_uint(_WAIT_FLAGS[mode]))
+    if rc != 0:
+        raise RuntimeError(f"hipSetDeviceFlags({mode}) failed with hipError {rc}")
+    return mode
 
 
 def native_enabled() -> bool:

@@ -33,6 +33,12 @@ COMMON_FLAGS = [
 ]
 
 
+# per-source flags: the fused step runs one wave per SIMD, nothing hides its
+# latencies but its own ILP -> the max-ILP machine scheduler (measured 4.83-4.91
+# vs 5.08 us/step with the default occupancy-driven one, docs/perf_notes.md)
+SOURCE_FLAGS = {"mlp_train.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and Path(cand).exists():
@@ -59,13 +65,43 @@ def _compile(src: Path, verbose: bool) -> Path:
     obj = OBJDIR / (src.stem + ".o")
     if not _stale(obj, [src, *_headers(), Path(__file__)]):
         return obj
-    cmd = [hipcc(), *COMMON_FLAGS, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+    cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
     return obj
+
+
+def variant(name: str, flags: list[str], sources: tuple[str, ...] = ("mlp_train.hip",),
+            verbose: bool = False) -> Path:
+    """A/B build: ``sources`` recompiled with extra ``flags`` (e.g. ``-DDTP_BWD_PK=0``)
+    into ``_lib/var_<name>/libdtp.so``, linked with the default objects of every other
+    source.  Load it with ``DTP_LIB=<path>`` (``_native.LIB_PATH``)."""
+    build(verbose=verbose)
+    vdir = LIBDIR / f"var_{name}"
+    (vdir / "obj").mkdir(parents=True, exist_ok=True)
+    objs = []
+    for src in _sources():
+        if src.name in sources:
+            obj = vdir / "obj" / (src.stem + ".o")
+            cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), *flags, "-I", str(CSRC), "-c", str(src),
+                   "-o", str(obj)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {src.name} ({name}):\n{r.stdout}\n{r.stderr}")
+            objs.append(obj)
+        else:
+            objs.append(OBJDIR / (src.stem + ".o"))
+    lib = vdir / "libdtp.so"
+    r = subprocess.run([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed ({name}):\n{r.stdout}\n{r.stderr}")
+    return lib
 
 
 def build(verbose: bool = False, jobs: int | None = None) -> Path:
@@ -92,12 +128,16 @@ def asm(src_name: str, out_dir: Path | None = None) -> Path:
     out_dir = out_dir or (LIBDIR / "asm")
     out_dir.mkdir(parents=True, exist_ok=True)
     src = CSRC / src_name
-    cmd = [hipcc(), *COMMON_FLAGS, "-I", str(CSRC), "--cuda-device-only", "-S", str(src),
+    cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), "-I", str(CSRC), "--cuda-device-only", "-S", str(src),
            "-o", str(out_dir / (src.stem + ".s"))]
     subprocess.run(cmd, check=True)
     return out_dir / (src.stem + ".s")
 
 
 if __name__ == "__main__":
-    p = build(verbose="-v" in sys.argv)
-    print(p)
+    # python -m distributed_training_pytorch_amd.build [-v] [--variant NAME FLAG...]
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(variant(sys.argv[i + 1], sys.argv[i + 2:], verbose="-v" in sys.argv))
+    else:
+        print(build(verbose="-v" in sys.argv))

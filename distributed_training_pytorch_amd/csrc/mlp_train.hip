@@ -14,6 +14,7 @@
 
 #include "dtp_api.h"
 #include "mlp_core.h"
+#include "mlp_pipe.h"
 #include "mlp_scalar.h"
 #include "optim_core.h"
 #include "xgmi_core.h"
@@ -29,6 +30,10 @@ constexpr int kAdamTab = 1024;
 #ifndef DTP_SCALAR_FWD
 #define DTP_SCALAR_FWD 0
 #endif
+#ifndef DTP_PIPE
+#define DTP_PIPE 1  // software-pipelined forward/backward (mlp_pipe.h); 0 = the v5 schedule
+#endif
+
 constexpr int kWaves = kBlock / kWave;
 
 template <class S>
@@ -72,8 +77,16 @@ struct SampleRegs {
 // Weights live in SGPRs (mlp_scalar.h), activations in VGPRs, the dW reduction
 // over the batch runs on MFMA through a per-wave LDS staging area, the optimizer
 // owns NPT parameters per thread in registers (params and moments).
+#ifndef DTP_TRAIN_WAVES_PER_EU
+#define DTP_TRAIN_WAVES_PER_EU 1  // one wave per SIMD: the scheduler may spend registers on latency
+#endif
+#if DTP_TRAIN_WAVES_PER_EU
+#define DTP_TRAIN_ATTR __attribute__((amdgpu_waves_per_eu(DTP_TRAIN_WAVES_PER_EU, DTP_TRAIN_WAVES_PER_EU)))
+#else
+#define DTP_TRAIN_ATTR
+#endif
 template <class S, int MODE, bool PROF = false>
-__global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
+__global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT;
   static_assert(NT * 256 <= 2 * 2 * kStgArr, "a wave's reduction tiles must fit in its staging area");
@@ -83,6 +96,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
   constexpr bool kUpdate = MODE != DTP_MODE_GRAD;
   // forward weights: SGPR stream from the global workspace (mlp_scalar.h) or LDS blocks
   constexpr bool kScalarFwd = DTP_SCALAR_FWD;
+  constexpr bool kPipe = DTP_PIPE && !DTP_SCALAR_FWD && S::NL >= 3;
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
@@ -204,7 +218,14 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       const bool valid = smpl.valid;
       float h[NL + 1][16];
       static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = smpl.x[decltype(IC)::value]; });
-      if constexpr (kScalarFwd) {
+      BBlk<S, NL - 1> pbt;  // backward blocks prefetched by the pipelined forward
+      TopB2<S> pbt2;
+      if constexpr (kPipe) {
+        FBlk<S, 0> pb0;
+        pb0.template load<0, FBlk<S, 0>::NR>(sm.wb);
+        if (c0 == 0) DTP_STAMP(1);
+        pipe_forward<S, 0>(sm.wb, pb0, h, slope, pbt, pbt2);
+      } else if constexpr (kScalarFwd) {
         if (c0 == 0) w = fresh_weights<SC::NLINES>(ws);
         if (c0 == 0) DTP_STAMP(1);
         scal_forward<S>(w, h, slope);
@@ -245,6 +266,10 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
       if (c0 == 0) DTP_STAMP(2);
 
       // ---------------- backward: dX chain (VALU, SGPR weights) + dW tiles (MFMA, K = samples)
+      if constexpr (kPipe) {
+        const PipeBwdCtx<S> pc{sm.wb, stg_pack, &sm.stage[wave][1][0], lane, slope, lpart};
+        pipe_backward<S>(pc, pbt, pbt2, h, dz, acc);
+      } else {
       static_for<0, NL>([&](auto RC) {
         constexpr int l = NL - 1 - decltype(RC)::value;
         constexpr int I = S::din(l), O = S::dout(l);
@@ -280,6 +305,7 @@ __global__ __launch_bounds__(kBlock) void mlp_train_kernel(DtpTrainArgs a) {
         __builtin_amdgcn_wave_barrier();
         acc[0] = wave_outer_acc(stg_pack, stg_pack + kStgArr, acc[0], lane);
         __builtin_amdgcn_wave_barrier();
+      }
       }
     }
     DTP_STAMP(8 + wave);
