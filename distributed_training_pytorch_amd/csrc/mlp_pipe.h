@@ -86,8 +86,10 @@ DTP_DEV void prefetch_chunk(const float* __restrict__ wl, P1& p1, P2& p2) {
 template <class S>
 using TopB2 = std::conditional_t<(S::NL >= 3), BBlk<S, (S::NL >= 3 ? S::NL - 2 : 1)>, NoBlk>;
 
-// one forward layer from the register block B, prefetching P1 ++ P2 row by row
-template <class S, int l, class P1, class P2>
+// one forward layer from the register block B, prefetching P1 ++ P2 row by row.
+// LM: LeakyReLU as max(z, slope * z), exact (NaN and signed zeros included) for
+// 0 <= slope <= 1 and one VALU op shorter than the compare-and-select form
+template <class S, int l, bool LM, class P1, class P2>
 DTP_DEV void pipe_fwd_layer(const float* __restrict__ wl, const FBlk<S, l>& B, float (&h)[S::NL + 1][16],
                             float slope, P1& p1, P2& p2) {
   constexpr int I = S::din(l), O = S::dout(l), NQ = FBlk<S, l>::NQ;
@@ -115,22 +117,22 @@ DTP_DEV void pipe_fwd_layer(const float* __restrict__ wl, const FBlk<S, l>& B, f
   static_for<0, O>([&](auto JC) {
     constexpr int j = decltype(JC)::value;
     const float v = (j & 1) ? z[j / 2].y : z[j / 2].x;
-    h[l + 1][j] = S::act(l) ? leaky(v, slope) : v;
+    h[l + 1][j] = S::act(l) ? (LM ? fmaxf(v, v * slope) : leaky(v, slope)) : v;
   });
 }
 
 // forward of layers [l, NL) with layer l's block in B; the last layer prefetches
 // the backward blocks of layers NL-1 and NL-2 into bt, bt2
-template <class S, int l>
+template <class S, int l, bool LM = false>
 DTP_DEV void pipe_forward(const float* __restrict__ wl, const FBlk<S, l>& B, float (&h)[S::NL + 1][16], float slope,
                           BBlk<S, S::NL - 1>& bt, TopB2<S>& bt2) {
   if constexpr (l + 1 < S::NL) {
     FBlk<S, l + 1> nb;
     NoBlk none;
-    pipe_fwd_layer<S, l>(wl, B, h, slope, nb, none);
-    pipe_forward<S, l + 1>(wl, nb, h, slope, bt, bt2);
+    pipe_fwd_layer<S, l, LM>(wl, B, h, slope, nb, none);
+    pipe_forward<S, l + 1, LM>(wl, nb, h, slope, bt, bt2);
   } else {
-    pipe_fwd_layer<S, l>(wl, B, h, slope, bt, bt2);
+    pipe_fwd_layer<S, l, LM>(wl, B, h, slope, bt, bt2);
   }
 }
 

@@ -10,6 +10,7 @@
 //   mlp_stage_fwd/bwd : one stage of a layer-split model (autograd path,
 //                       demo_one_model_multi_gpu.py:17-42 equivalent).
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "dtp_api.h"
@@ -85,7 +86,11 @@ struct SampleRegs {
 #else
 #define DTP_TRAIN_ATTR
 #endif
-template <class S, int MODE, bool PROF = false>
+// FAST: the common configuration fixed at compile time (device shuffle sampler,
+// power-of-two dataset cached in LDS, 0 <= slope <= 1; fast_path_ok() on the host):
+// the next step's sample gather is straight-line LDS code the scheduler can
+// interleave with the optimizer, and LeakyReLU is max(z, slope z).
+template <class S, int MODE, bool PROF = false, bool FAST = false>
 __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT;
@@ -110,7 +115,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   float* __restrict__ gp = a.params + (size_t)model * P;
   float* __restrict__ ws = a.wsp + (size_t)model * SC::WS;
   const SamplerCfg smp = a.smp;
-  const bool cached = a.cache_data && smp.n * (S::IN + ydim) <= kDataCache;
+  const bool cached = FAST || (a.cache_data && smp.n * (S::IN + ydim) <= kDataCache);
   int pf[NPT], pb[NPT], tp[NPT], pfl[NPT];
   float pw[NPT], mr[NPT], vr[NPT];
 #pragma unroll
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     }
   }
   // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
-  const bool explicit_idx = smp.mode == SAMPLER_EXPLICIT;
+  const bool explicit_idx = !FAST && smp.mode == SAMPLER_EXPLICIT;
   int epoch = explicit_idx ? 0 : t0 / smp.steps_per_epoch;
   int bi = explicit_idx ? 0 : t0 - epoch * smp.steps_per_epoch;
   int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
@@ -159,6 +164,25 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   auto gather = [&](int it_, const BatchPos& bp_, const uint32_t (&keys_)[4], int k, int bsz_) {
     SampleRegs<S> r;
     r.valid = k < bsz_;
+    if constexpr (FAST) {
+      // position in the padded list (padding repeats from the start), then the
+      // one-pass permutation of a power-of-two domain: no branches
+      int q = smp.rank + (bp_.start + k) * smp.world;
+      q = q >= smp.n ? q - smp.n : q;
+      int di = (int)feistel_permute_pow2((uint32_t)q, smp.bits, keys_);
+      di = r.valid ? di : 0;
+      static_for<0, S::IN>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        const float v = sm.data[di * S::IN + i];
+        r.x[i] = r.valid ? v : 0.f;
+      });
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float v = j < ydim ? sm.data[yoff + di * ydim + j] : 0.f;
+        r.y[j] = r.valid ? v : 0.f;
+      });
+      return r;
+    }
     int di = 0;
     if (r.valid) di = explicit_idx ? a.idx[(size_t)it_ * smp.batch + k] : sample_index(smp, bp_, keys_, k);
     static_for<0, S::IN>([&](auto IC) {
@@ -224,7 +248,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
         FBlk<S, 0> pb0;
         pb0.template load<0, FBlk<S, 0>::NR>(sm.wb);
         if (c0 == 0) DTP_STAMP(1);
-        pipe_forward<S, 0>(sm.wb, pb0, h, slope, pbt, pbt2);
+        pipe_forward<S, 0, FAST>(sm.wb, pb0, h, slope, pbt, pbt2);
       } else if constexpr (kScalarFwd) {
         if (c0 == 0) w = fresh_weights<SC::NLINES>(ws);
         if (c0 == 0) DTP_STAMP(1);
@@ -355,19 +379,18 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid);
     }
 
-    if (tid == 0 && a.loss_log) {
-      const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
-      a.loss_log[(size_t)lslot * a.n_models + model] = lg;
-    }
     // advance the sampler / loss-ring position and gather the next step's first
     // chunk now: its index hashing and LDS reads overlap the optimizer's latency
+    // (FAST: the gather is straight-line code in the optimizer's basic block; the
+    // loss-log store, a branch of thread 0, comes after the update)
+    const int lslot_now = lslot;
     if (!explicit_idx && ++bi == smp.steps_per_epoch) {
       bi = 0;
       ++epoch;
       epoch_keys(smp, epoch, keys);
     }
     if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
-    if (it + 1 < a.n_steps) {
+    if (FAST || it + 1 < a.n_steps) {  // FAST gathers past the last step too (harmless LDS reads)
       const BatchPos bpn = batch_at(epoch, bi);
       nxt = gather(it + 1, bpn, keys, tid, bpn.size);
     }
@@ -398,6 +421,10 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
         *(own ? &sm.wb[pfl[k]] : &sm.sink[0]) = pw[k];
         *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
       }
+    }
+    if (tid == 0 && a.loss_log) {
+      const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
+      a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
     }
     DTP_STAMP(6);
     if (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight stores reached L2 before the barrier
@@ -448,27 +475,44 @@ using dtp::set_err;
 
 using TrainLaunchFn = void (*)(const DtpTrainArgs&, hipStream_t);
 
-template <class S, int MODE>
+template <class S, int MODE, bool FAST = false>
 void launch_mode(const DtpTrainArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dtp::mlp_train_kernel<S, MODE>), dim3(a.n_models), dim3(dtp::kBlock), 0, st, a);
+  hipLaunchKernelGGL((dtp::mlp_train_kernel<S, MODE, false, FAST>), dim3(a.n_models), dim3(dtp::kBlock), 0, st, a);
 }
 
-// the kernel instance of (shape S, mode), resolved once (the native engine keeps it)
+// the kernel instance of (shape S, mode, fast path), resolved once (the native
+// engine keeps it); the FAST instances exist for the Adam modes (the training
+// configurations of the demos and bench.py)
 template <class S>
-TrainLaunchFn train_fn(int mode) {
+TrainLaunchFn train_fn(int mode, bool fast) {
   switch (mode) {
     case DTP_MODE_GRAD: return &launch_mode<S, DTP_MODE_GRAD>;
-    case DTP_MODE_ADAM: return &launch_mode<S, DTP_MODE_ADAM>;
+    case DTP_MODE_ADAM: return fast ? &launch_mode<S, DTP_MODE_ADAM, true> : &launch_mode<S, DTP_MODE_ADAM>;
     case DTP_MODE_SGD: return &launch_mode<S, DTP_MODE_SGD>;
-    case DTP_MODE_XGMI_ADAM: return &launch_mode<S, DTP_MODE_XGMI_ADAM>;
+    case DTP_MODE_XGMI_ADAM:
+      return fast ? &launch_mode<S, DTP_MODE_XGMI_ADAM, true> : &launch_mode<S, DTP_MODE_XGMI_ADAM>;
     case DTP_MODE_XGMI_SGD: return &launch_mode<S, DTP_MODE_XGMI_SGD>;
     default: return nullptr;
   }
 }
 
-TrainLaunchFn resolve_train(int in, int h, int nl, int out, int mode) {
+// may this launch take the FAST instance?  (the kernel's FAST preconditions)
+bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
+  static const bool disabled = [] {
+    const char* e = getenv("DTP_FAST");
+    return e && e[0] == '0';
+  }();
+  if (disabled || (mode != DTP_MODE_ADAM && mode != DTP_MODE_XGMI_ADAM)) return false;
+  const dtp::SamplerCfg& s = a.smp;
+  const int ydim = a.loss == DTP_LOSS_CE ? 1 : out;
+  return a.cache_data && s.mode == dtp::SAMPLER_DIST_SHUFFLE && s.bits >= 1 && s.bits < 31 && s.n == (1 << s.bits) &&
+         s.n * (in + ydim) <= dtp::kDataCache && a.hp.slope >= 0.f && a.hp.slope <= 1.f;
+}
+
+TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode) {
+  const bool fast = fast_path_ok(a, in, out, mode);
 #define X(I, H, N, O) \
-  if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false>>(mode);
+  if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false>>(mode, fast);
   DTP_TRAIN_SHAPES(X)
 #undef X
   return nullptr;
@@ -506,7 +550,10 @@ struct TrainEngine {
 
 template <class S>
 int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
-  hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_ADAM, true>), dim3(a->n_models), dim3(dtp::kBlock), 0, st, *a);
+  if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM))
+    return set_err(-2, "the profile instance is the FAST one: power-of-two cached dataset, shuffle sampler");
+  hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_ADAM, true, true>), dim3(a->n_models), dim3(dtp::kBlock), 0,
+                     st, *a);
   return check_launch("mlp_train_kernel<prof>");
 }
 
@@ -535,7 +582,7 @@ int dtp_mlp_param_count(int in, int h, int nl, int out) {
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream) {
   if (int rc = validate_train(a, mode)) return rc;
   if (mode == DTP_MODE_GRAD && a->n_steps != 1) return set_err(-4, "MODE_GRAD requires n_steps == 1");
-  TrainLaunchFn fn = resolve_train(in, h, nl, out, mode);
+  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode);
   if (!fn) return set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
   fn(*a, (hipStream_t)stream);
   return check_launch("mlp_train_kernel");
@@ -543,7 +590,7 @@ int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mod
 
 void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
   if (validate_train(a, mode)) return nullptr;
-  TrainLaunchFn fn = resolve_train(in, h, nl, out, mode);
+  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode);
   if (!fn) {
     set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
     return nullptr;

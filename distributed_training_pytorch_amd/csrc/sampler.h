@@ -69,6 +69,21 @@ DTP_HD uint32_t feistel_permute(uint32_t q, uint32_t n, int bits, const uint32_t
   return q;
 }
 
+// feistel_permute for n == 2^bits: one pass lands in [0, n), no cycle-walk loop
+// (straight-line code the scheduler can interleave with other work)
+DTP_HD uint32_t feistel_permute_pow2(uint32_t q, int bits, const uint32_t (&k)[4]) {
+  const int r = bits > 1 ? (bits >> 1) : 1;
+  const uint32_t rmask = (1u << r) - 1u;
+  const uint32_t dmask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t hi = q >> r;
+    const uint32_t lo = (q & rmask) ^ (hash32(hi ^ k[i]) & rmask);
+    q = ((lo << (bits - r)) | hi) & dmask;
+  }
+  return q;
+}
+
 // Batch geometry of global step t on this rank.
 struct BatchPos {
   int epoch;

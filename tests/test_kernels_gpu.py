@@ -142,6 +142,48 @@ def test_fused_trainer_large_dataset(n, cache):
     tr.close()
 
 
+_FAST_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.toy_data import ToyData
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
+from distributed_training_pytorch_amd.ops.optim import OptimConfig
+dev = torch.device("cuda", 0)
+X, Y = ToyData(n={n}, seed=8).device_tensors(dev)
+g = torch.Generator().manual_seed(0)
+init = [(torch.randn(TOY_SPEC.P, generator=g) * 0.4).to(dev) for _ in range(2)]
+tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n={n}, batch=256, seed=4), OptimConfig(lr=1e-2),
+                  EngineConfig(steps_per_launch=7), init_params=init)
+tr.train(19)
+tr.synchronize()
+torch.save({{"p": tr.params.cpu(), "l": tr.losses(0, 19)}}, {out!r})
+"""
+
+
+@pytest.mark.parametrize("n", [512, 500])
+def test_fast_instance_bitwise_equals_generic(n, tmp_path):
+    """The FAST kernel instance (power-of-two cached dataset, shuffle sampler) and the
+    generic one (DTP_FAST=0) give bitwise-identical weights and losses; n = 500 has no
+    FAST instance (cycle-walking sampler) and must match itself either way."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for flag in ("1", "0"):
+        out = str(tmp_path / f"fast{flag}.pt")
+        env = dict(os.environ, DTP_FAST=flag)
+        r = subprocess.run([sys.executable, "-c", _FAST_SCRIPT.format(root=root, n=n, out=out)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[flag] = torch.load(out, weights_only=True)
+    assert torch.equal(outs["1"]["p"], outs["0"]["p"])
+    assert torch.equal(outs["1"]["l"], outs["0"]["l"])
+
+
 def test_fused_trainer_torch_sampler_order():
     ds = ToyData(seed=3)
     X, Y = ds.device_tensors(DEV)
