@@ -86,8 +86,9 @@ struct SampleRegs {
 #else
 #define DTP_TRAIN_ATTR
 #endif
-// FAST: the common configuration fixed at compile time (device shuffle sampler,
-// power-of-two dataset cached in LDS, 0 <= slope <= 1; fast_path_ok() on the host):
+// FAST: the common configuration fixed at compile time (MSE, batch <= 256, device
+// shuffle sampler, power-of-two dataset cached in LDS, 0 <= slope <= 1;
+// fast_path_ok() on the host):
 // the next step's sample gather is straight-line LDS code the scheduler can
 // interleave with the optimizer, and LeakyReLU is max(z, slope z).
 template <class S, int MODE, bool PROF = false, bool FAST = false>
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
-  const bool ce = a.loss == DTP_LOSS_CE;
+  const bool ce = !FAST && a.loss == DTP_LOSS_CE;  // FAST: MSE
   const int ydim = ce ? 1 : S::OUT;
   const float slope = a.hp.slope;
 
@@ -227,17 +228,14 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     const BatchPos bp = batch_at(epoch, bi);
     const int bsz = bp.size;
     const float inv = ce ? 1.f / (float)bsz : 1.f / (float)(bsz * S::OUT);
-    // this step's optimizer scalars, off the critical path (overlaps the forward)
-    if (kAdam && it > 0 && it % kAdamTab == 0) {  // ordered by the step's barriers before its use
-      __syncthreads();
-      fill_adam(it);
-    }
 
     f32x4 acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int c0 = 0; c0 < bsz; c0 += kBlock) {
+    // FAST: batch <= kBlock, one chunk (the loop folds away: fwd, loss and bwd are
+    // one straight-line region)
+    for (int c0 = 0; c0 < (FAST ? kBlock : bsz); c0 += kBlock) {
       const SampleRegs<S> smpl = c0 == 0 ? nxt : gather(it, bp, keys, c0 + tid, bsz);
       const bool valid = smpl.valid;
       float h[NL + 1][16];
@@ -429,6 +427,12 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     DTP_STAMP(6);
     if (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight stores reached L2 before the barrier
     __syncthreads();  // updated weights visible; reduction tiles consumed
+    // the next kAdamTab steps' Adam scalars, once every kAdamTab steps at a step
+    // boundary (every wave read this step's entry before the barrier above)
+    if (kAdam && (it + 1) % kAdamTab == 0 && it + 1 < a.n_steps) {
+      fill_adam(it + 1);
+      __syncthreads();
+    }
     DTP_STAMP(7);
   }
 
@@ -505,8 +509,9 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   if (disabled || (mode != DTP_MODE_ADAM && mode != DTP_MODE_XGMI_ADAM)) return false;
   const dtp::SamplerCfg& s = a.smp;
   const int ydim = a.loss == DTP_LOSS_CE ? 1 : out;
-  return a.cache_data && s.mode == dtp::SAMPLER_DIST_SHUFFLE && s.bits >= 1 && s.bits < 31 && s.n == (1 << s.bits) &&
-         s.n * (in + ydim) <= dtp::kDataCache && a.hp.slope >= 0.f && a.hp.slope <= 1.f;
+  return a.cache_data && a.loss == DTP_LOSS_MSE && s.batch <= dtp::kBlock && s.mode == dtp::SAMPLER_DIST_SHUFFLE &&
+         s.bits >= 1 && s.bits < 31 && s.n == (1 << s.bits) && s.n * (in + ydim) <= dtp::kDataCache &&
+         a.hp.slope >= 0.f && a.hp.slope <= 1.f;
 }
 
 TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode) {

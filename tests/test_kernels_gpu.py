@@ -184,6 +184,23 @@ def test_fast_instance_bitwise_equals_generic(n, tmp_path):
     assert torch.equal(outs["1"]["l"], outs["0"]["l"])
 
 
+def test_adam_table_refill_inside_one_launch():
+    """A persistent launch longer than the kernel's Adam-scalar table (1024 steps)
+    refills it at a step boundary: bitwise equal to short launches."""
+    X, Y = ToyData(seed=6).device_tensors(DEV)
+    init = [_params(TOY_SPEC, 50 + i, 0.4) for i in range(2)]
+    res = []
+    for spl in (1100, 100):
+        tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=256, seed=1), OptimConfig(lr=1e-3),
+                          EngineConfig(steps_per_launch=spl), init_params=init)
+        tr.train(1100)
+        tr.synchronize()
+        res.append((tr.params.clone(), tr.losses(0, 1100)))
+        tr.close()
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 def test_fused_trainer_torch_sampler_order():
     ds = ToyData(seed=3)
     X, Y = ds.device_tensors(DEV)
