@@ -36,7 +36,10 @@ COMMON_FLAGS = [
 # per-source flags: the fused step runs one wave per SIMD, nothing hides its
 # latencies but its own ILP -> the max-ILP machine scheduler (measured 4.83-4.91
 # vs 5.08 us/step with the default occupancy-driven one, docs/perf_notes.md)
-SOURCE_FLAGS = {"mlp_train.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# -ffp-contract=off where the optimizer math lives: every fused multiply-add there is
+# an explicit fmaf, so kernel instances scheduled differently round identically
+SOURCE_FLAGS = {"mlp_train.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-ffp-contract=off"],
+                "optim.hip": ["-ffp-contract=off"]}
 
 
 def hipcc() -> str:

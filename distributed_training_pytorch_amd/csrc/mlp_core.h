@@ -194,6 +194,9 @@ DTP_DEV f32x4 wave_outer_acc(const float* __restrict__ dzb, const float* __restr
     a[i] = a4[i];
     b[i] = b4[i];
   }
+  // all eight reads in flight before the first MFMA waits (left alone, the
+  // scheduler pairs each read with its MFMAs: four LDS round trips in a row)
+  __builtin_amdgcn_sched_barrier(0);
   f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
         static_for<0, S::OUT>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
           const float d = h[L + 1][j] - smpl.y[j];
-          lpart += valid ? d * d : 0.f;
+          lpart = valid ? fmaf(d, d, lpart) : lpart;
           dz[j] = valid ? 2.f * d * inv : 0.f;
         });
       } else {
@@ -382,7 +382,12 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     // (FAST: the gather is straight-line code in the optimizer's basic block; the
     // loss-log store, a branch of thread 0, comes after the update)
     const int lslot_now = lslot;
-    if (!explicit_idx && ++bi == smp.steps_per_epoch) {
+    if constexpr (FAST) {  // branch-free: the epoch keys are re-derived every step (scalar unit)
+      const bool roll = ++bi == smp.steps_per_epoch;
+      bi = roll ? 0 : bi;
+      epoch += roll ? 1 : 0;
+      epoch_keys(smp, epoch, keys);
+    } else if (!explicit_idx && ++bi == smp.steps_per_epoch) {
       bi = 0;
       ++epoch;
       epoch_keys(smp, epoch, keys);

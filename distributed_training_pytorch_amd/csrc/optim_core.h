@@ -56,21 +56,26 @@ DTP_DEV AdamScalars adam_consts(const DtpHyper& hp) {
   return s;
 }
 
+// Every fused multiply-add is spelled out (fmaf) and the translation units that
+// use these helpers build with -ffp-contract=off (build.py), so the rounding of
+// each update is fixed by the source, not by how the compiler scheduled the
+// surrounding kernel: every kernel instance (FAST or generic, fused step or flat
+// optimizer) produces bitwise the same update.
 DTP_DEV void adam_update(float& p, float& m, float& v, float g, const AdamScalars& s) {
-  if (s.wd != 0.f) g = g + s.wd * p;
-  m = m + s.one_m_b1 * (g - m);
-  v = v * s.b2 + s.one_m_b2 * g * g;
+  if (s.wd != 0.f) g = fmaf(s.wd, p, g);
+  m = fmaf(s.one_m_b1, g - m, m);                  // m.lerp_(g, 1 - b1)
+  v = fmaf(s.one_m_b2 * g, g, v * s.b2);           // v.mul_(b2).addcmul_(g, g, 1 - b2)
   const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
-  p = p - s.step_size * (m / denom);
+  p = fmaf(-s.step_size, m / denom, p);            // p.addcdiv_(m, denom, -step_size)
 }
 
 DTP_DEV void sgd_update(float& p, float& buf, float g, float lr, float mom, float wd, bool first) {
-  if (wd != 0.f) g = g + wd * p;
+  if (wd != 0.f) g = fmaf(wd, p, g);
   if (mom != 0.f) {
-    buf = first ? g : buf * mom + g;
+    buf = first ? g : fmaf(buf, mom, g);
     g = buf;
   }
-  p = p - lr * g;
+  p = fmaf(-lr, g, p);
 }
 
 }  // namespace dtp
