@@ -42,3 +42,29 @@ def test_runner_reports_phases(tmp_path):
         assert {"data", "forward", "backward+allreduce", "optimizer"} <= set(summary["phases"])
     finally:
         profiling.set_enabled(False)
+
+
+def test_wait_mode_knob(monkeypatch):
+    """DTP_WAIT_MODE: 'auto' leaves the HIP runtime alone (no GPU touched); an unknown
+    mode is rejected before anything is called."""
+    import pytest
+
+    from distributed_training_pytorch_amd import _native as nat
+
+    monkeypatch.delenv("DTP_WAIT_MODE", raising=False)
+    assert nat.set_wait_mode() == "auto"
+    monkeypatch.setenv("DTP_WAIT_MODE", "nope")
+    with pytest.raises(ValueError):
+        nat.set_wait_mode()
+
+
+def test_build_flags_pin_fused_step_numerics():
+    """The fused step and the flat optimizer build with -ffp-contract=off (their
+    fmaf-explicit math must round the same in every kernel instance) and the step
+    with the max-ILP scheduler; nothing else inherits those flags."""
+    from distributed_training_pytorch_amd import build
+
+    assert "-ffp-contract=off" in build.SOURCE_FLAGS["mlp_train.hip"]
+    assert "-ffp-contract=off" in build.SOURCE_FLAGS["optim.hip"]
+    assert "-amdgpu-sched-strategy=max-ilp" in build.SOURCE_FLAGS["mlp_train.hip"]
+    assert "gemm.hip" not in build.SOURCE_FLAGS
