@@ -169,6 +169,7 @@ def _declare(lib):
         "dtp_mlp_workspace_floats": (c_int, [c_int] * 4),
         "dtp_mlp_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
+        "dtp_xgmi_fused_buffer_bytes": (c_longlong, [c_int, c_int, c_int]),
         "dtp_train_engine_create": (c_void_p, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
         "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_void_p]),
         "dtp_train_engine_destroy": (None, [c_void_p]),

@@ -54,6 +54,7 @@ int dtp_mlp_param_count(int in, int h, int nl, int out);
 int dtp_mlp_workspace_floats(int in, int h, int nl, int out);
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream);
 int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream);
+long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world);
 
 // ---- stage forward / backward (autograd path, layer-split pipeline) ----
 struct DtpStageArgs {

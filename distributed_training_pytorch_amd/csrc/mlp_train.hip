@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   float pw[NPT], mr[NPT], vr[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int p = tid + k * kBlock;
+    const int p = NPT * tid + k;  // blocked ownership: thread t holds parameters NPT t .. NPT t + NPT-1
     scal_pos<S>(p < P ? p : 0, pf[k], pb[k], tp[k], pfl[k]);
     const bool own = p < P;
     pw[k] = own ? gp[p] : 0.f;
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   __syncthreads();  // weight blocks zeroed (pads stay 0) before the owners scatter into them
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    if (tid + k * kBlock < P) {
+    if (NPT * tid + k < P) {
       if (kScalarFwd) ws[pf[k]] = pw[k];
       sm.wb[pfl[k]] = pw[k];
       if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     if constexpr (MODE == DTP_MODE_GRAD) {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        const int p = tid + k * kBlock;
+        const int p = NPT * tid + k;
         if (p < P) a.grad_out[(size_t)model * P + p] = g[k] * a.hp.grad_scale;
       }
       if (tid == 0) a.grad_out[(size_t)a.n_models * P + model] = mean_loss;
@@ -419,13 +419,14 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       }
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        const bool own = tid + k * kBlock < P;
+        const bool own = NPT * tid + k < P;
         if (kScalarFwd && own) ws[pf[k]] = pw[k];
         *(own ? &sm.wb[pfl[k]] : &sm.sink[0]) = pw[k];
         *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
       }
     }
-    if (tid == 0 && a.loss_log) {
+    // the thread that holds the global loss logs it (xgmi_core.h: the loss granule's owner)
+    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, kBlock) : 0) && a.loss_log) {
       const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
       a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
     }
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   if constexpr (kUpdate) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int p = tid + k * kBlock;
+      const int p = NPT * tid + k;
       if (p < P) {
         gp[p] = pw[k];
         a.opt_m[(size_t)model * P + p] = mr[k];
@@ -578,6 +579,13 @@ int dtp_mlp_workspace_floats(int in, int h, int nl, int out) {
   DTP_TRAIN_SHAPES(X)
 #undef X
   return 0;
+}
+
+// bytes of one rank's receive buffer of the fused step's xGMI exchange
+// ([parity 2][model][src rank][slot] of 16-byte granules, xgmi_core.h)
+long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world) {
+  const int npt = (P + dtp::kBlock - 1) / dtp::kBlock;
+  return 2ll * n_models * world * dtp::xgmi_slot16(P, npt) * 16ll;
 }
 
 int dtp_mlp_param_count(int in, int h, int nl, int out) {

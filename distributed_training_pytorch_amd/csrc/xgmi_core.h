@@ -5,13 +5,14 @@
 // Guideline 16 recipe R2, extended to the system scope):
 //   * every rank owns a receive buffer in fine-grained, uncached device memory
 //     (hipExtMallocWithFlags(hipDeviceMallocUncached)), IPC-mapped into every
-//     other rank;  layout [parity 2][model][src rank][slot] of 8-byte granules;
-//   * a granule is {tag = exchange epoch (32 bit), value = fp32 bits}, written by
-//     ONE 8-byte system-scope store, so it can never be observed torn and needs
-//     no separate flag or fence: the consumer polls each granule until its tag
-//     equals the epoch it expects;
+//     other rank;  layout [parity 2][model][src rank][slot] of 16-byte granules;
+//   * a granule is {tag = exchange epoch, two fp32 values, check word}, written
+//     by ONE 16-byte system-scope store; it needs no separate flag or fence: the
+//     consumer polls each granule until its tag equals the epoch it expects and
+//     its check word matches (a torn granule fails the check and is re-polled);
 //   * PUSH: each rank stores its slot into every peer's buffer (posted xGMI
-//     writes over all 7 links in parallel), then reads only its LOCAL buffer;
+//     writes over all 7 links in parallel), then reads only its LOCAL buffer
+//     (its own contribution stays in registers);
 //   * two parities: a fast rank can be at most one exchange ahead of a slow one
 //     (it cannot finish exchange e+1 before the slow rank published e+1), so
 //     exchange e+1 never overwrites slots still being read for exchange e;
@@ -41,68 +42,112 @@ DTP_DEV unsigned long long load_granule_sys(const unsigned long long* p) {
 // largest world the in-kernel exchange serves (one node: 8 GPUs, 7 xGMI links each)
 constexpr int kXgmiMaxWorld = 8;
 
-// granules per (model, src rank) slot: P gradient values + 1 loss, 64-byte rounded
-DTP_HD int xgmi_slot_granules(int P) { return (P + 1 + 7) & ~7; }
+// ---- fused-step exchange: 16-byte granules -----------------------------------
+// The fused train step owns its parameters in blocks: thread t holds parameters
+// NPT*t .. NPT*t + NPT-1 (P = total).  Each thread publishes its NPT gradient values
+// as ceil(NPT/2) granules of 16 bytes {epoch, v0, v1, check}; the global mean loss
+// rides in one more granule (thread xgmi_loss_tid).  A granule is written by ONE
+// 16-byte system-scope store and accepted only when its tag equals the expected
+// epoch AND its check word matches the payload, so a reader can never use a torn
+// granule (a 16-byte store landing as two halves fails the check and is re-polled).
+// Half the transactions of one 8-byte {epoch, value} granule per value, and a rank's
+// own contribution never leaves its registers.  (Splitting the workgroup into
+// sender and receiver waves, so no poll waits behind the wave's own remote stores,
+// measured slower: two more barriers; branch exp/xgmi-split.)
+template <int NPT>
+DTP_HD constexpr int xgmi_gpt() { return (NPT + 1) / 2; }  // granules per thread
+DTP_HD constexpr int xgmi_nthr(int P, int npt) { return (P + npt - 1) / npt; }
+template <int NPT>
+DTP_HD constexpr int xgmi_loss_tid(int P, int nthreads) {
+  return xgmi_nthr(P, NPT) < nthreads ? xgmi_nthr(P, NPT) : 0;
+}
+// granules per (parity, model, source rank) slot, rounded to 64 bytes
+DTP_HD constexpr int xgmi_slot16(int P, int npt) { return (xgmi_nthr(P, npt) * ((npt + 1) / 2) + 1 + 3) & ~3; }
+
+DTP_DEV uint32_t xgmi_check(uint32_t e, uint32_t a, uint32_t b) {
+  return e ^ a ^ ((b << 13) | (b >> 19)) ^ 0x9E3779B9u;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSysCoherent = 17;  // buffer cache policy sc0 | sc1: system scope, no cache allocation
+
+DTP_DEV __amdgpu_buffer_rsrc_t xgmi_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
 
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
                                    unsigned epoch, int tid) {
+  constexpr int GPT = xgmi_gpt<NPT>();
   const int W = a.smp.world, R = a.smp.rank;
-  const int slot = xgmi_slot_granules(P);
-  const int par = (int)(epoch & 1u);
-  const size_t base = (size_t)(par * a.n_models + model) * W;
-  // publish our slot into every rank's buffer (our own included)
-  for (int r = 0; r < W; ++r) {
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.peers[r]) + (base + R) * slot;
+  const int slot = xgmi_slot16(P, NPT);
+  const int nthr = xgmi_nthr(P, NPT);
+  const int ltid = xgmi_loss_tid<NPT>(P, NTHREADS);
+  const size_t base = (size_t)((int)(epoch & 1u) * a.n_models + model) * W;
+  // this thread's granules: its gradient blocks (threads < nthr) and the loss (ltid)
+  const bool has_g = tid < nthr;
+  const bool has_l = tid == ltid;
+  float v[GPT + 1][2];
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int p = tid + k * NTHREADS;
-      if (p < P) store_granule_sys(dst + p, pack_granule(epoch, g[k]));
-    }
-    if (tid == 0) store_granule_sys(dst + P, pack_granule(epoch, loss));
+  for (int k = 0; k < GPT; ++k) {
+    v[k][0] = 2 * k < NPT ? g[2 * k] : 0.f;
+    v[k][1] = 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f;
   }
-  // consume every rank's slot from our local buffer: every granule this thread
-  // needs (W x (NPT + loss)) is requested at once and only the missing ones are
-  // re-polled, so an exchange costs ONE uncached round trip once the data is
-  // there, not W sequential ones; then sum in rank order 0..W-1 (bitwise
-  // identical on every rank)
-  const unsigned long long* mine = reinterpret_cast<const unsigned long long*>(a.peers[R]);
+  v[GPT][0] = loss;
+  v[GPT][1] = 0.f;
+  auto gidx = [&](int k) { return k < GPT ? tid * GPT + k : nthr * GPT; };  // granule index in a slot
+  auto mine_k = [&](int k) { return k < GPT ? has_g : has_l; };
+  // publish to every peer (posted xGMI writes; our own slot stays in registers)
+  for (int r = 0; r < W; ++r) {
+    if (r == R) continue;
+    const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(a.peers[r]);
+#pragma unroll
+    for (int k = 0; k <= GPT; ++k) {
+      if (!mine_k(k)) continue;
+      const uint32_t x0 = __float_as_uint(v[k][0]), x1 = __float_as_uint(v[k][1]);
+      const u32x4 q = {epoch, x0, x1, xgmi_check(epoch, x0, x1)};
+      __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(((base + R) * slot + gidx(k)) * 16), 0, kSysCoherent);
+    }
+  }
+  // consume every peer's granules from our local buffer: all pending ones requested
+  // at once, only the missing ones re-polled; bounded by the deadline
+  const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[R]);
   const unsigned long long deadline =
       __builtin_amdgcn_s_memrealtime() + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
-  // sticky failure: once any exchange of this rank timed out, later ones do not
-  // wait again (a persistent launch must not multiply the timeout by its steps)
   bool dead = a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
-  constexpr int NG = NPT + 1;  // + the loss granule (thread 0)
-  float val[kXgmiMaxWorld][NG];
-  static_assert(kXgmiMaxWorld * NG <= 64, "pending mask holds every (rank, granule) pair");
-  uint64_t pending = 0ull;  // bit r*NG + k: granule (r, k) still missing
+  float val[kXgmiMaxWorld][GPT + 1][2];
+  static_assert(kXgmiMaxWorld * (GPT + 1) <= 64, "pending mask holds every (rank, granule) pair");
+  uint64_t pending = 0ull;
 #pragma unroll
   for (int r = 0; r < kXgmiMaxWorld; ++r) {
 #pragma unroll
-    for (int k = 0; k < NG; ++k) {
-      val[r][k] = 0.f;
-      const int p = k < NPT ? tid + k * NTHREADS : P;
-      const bool mine_to_read = r < W && (k < NPT ? p < P : tid == 0);
-      if (mine_to_read) pending |= 1ull << (r * NG + k);
+    for (int k = 0; k <= GPT; ++k) {
+      val[r][k][0] = (r == R) ? v[k][0] : 0.f;
+      val[r][k][1] = (r == R) ? v[k][1] : 0.f;
+      if (r < W && r != R && mine_k(k)) pending |= 1ull << (r * (GPT + 1) + k);
     }
   }
   while (pending && !dead) {
-    unsigned long long x[kXgmiMaxWorld][NG];
+    u32x4 x[kXgmiMaxWorld][GPT + 1];
 #pragma unroll
     for (int r = 0; r < kXgmiMaxWorld; ++r) {
 #pragma unroll
-      for (int k = 0; k < NG; ++k) {
-        const int p = k < NPT ? tid + k * NTHREADS : P;
-        x[r][k] = (pending >> (r * NG + k)) & 1ull ? load_granule_sys(mine + (base + r) * slot + p) : 0ull;
+      for (int k = 0; k <= GPT; ++k) {
+        x[r][k] = u32x4{0u, 0u, 0u, 0u};
+        if ((pending >> (r * (GPT + 1) + k)) & 1ull)
+          x[r][k] = __builtin_amdgcn_raw_buffer_load_b128(ms, (int)(((base + r) * slot + gidx(k)) * 16), 0,
+                                                          kSysCoherent);
       }
     }
 #pragma unroll
     for (int r = 0; r < kXgmiMaxWorld; ++r) {
 #pragma unroll
-      for (int k = 0; k < NG; ++k) {
-        if (((pending >> (r * NG + k)) & 1ull) && (unsigned)(x[r][k] >> 32) == epoch) {
-          val[r][k] = __uint_as_float((unsigned)x[r][k]);
-          pending &= ~(1ull << (r * NG + k));
+      for (int k = 0; k <= GPT; ++k) {
+        const u32x4 q = x[r][k];
+        if (((pending >> (r * (GPT + 1) + k)) & 1ull) && q.x == epoch && q.w == xgmi_check(epoch, q.y, q.z)) {
+          val[r][k][0] = __uint_as_float(q.y);
+          val[r][k][1] = __uint_as_float(q.z);
+          pending &= ~(1ull << (r * (GPT + 1) + k));
         }
       }
     }
@@ -117,16 +162,17 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  float lacc = 0.f;
+  // sum in rank order 0..W-1 (bitwise identical on every rank; absent ranks add +0)
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     float acc = 0.f;
 #pragma unroll
-    for (int r = 0; r < kXgmiMaxWorld; ++r) acc += val[r][k];  // absent ranks contribute +0.0f
+    for (int r = 0; r < kXgmiMaxWorld; ++r) acc += val[r][k / 2][k & 1];
     g[k] = acc;
   }
+  float lacc = 0.f;
 #pragma unroll
-  for (int r = 0; r < kXgmiMaxWorld; ++r) lacc += val[r][NPT];
+  for (int r = 0; r < kXgmiMaxWorld; ++r) lacc += val[r][GPT][0];
   return lacc;
 }
 

@@ -27,6 +27,7 @@ from .. import _native as nat
 
 
 def slot_granules(P: int) -> int:
+    """8-byte granules per slot of the stand-alone all-reduce (XgmiAllReduce)."""
     return (P + 1 + 7) & ~7
 
 
@@ -101,7 +102,9 @@ class XgmiExchange:
         self.n_models = n_models
         self.P = P
         world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.bufs = PeerBuffers(2 * n_models * world * slot_granules(P) * 8, device, group)
+        # the fused kernel's 16-byte-granule layout, sized by the library itself
+        nbytes = nat.require(device).dtp_xgmi_fused_buffer_bytes(P, n_models, world)
+        self.bufs = PeerBuffers(nbytes, device, group)
         self.lib = self.bufs.lib
         self.world, self.rank = self.bufs.world, self.bufs.rank
         self.peer_table = self.bufs.peer_table
