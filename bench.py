@@ -105,15 +105,31 @@ def main():
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm}
 
+    # the timed region is bracketed by an all-rank barrier + synchronize on both sides;
+    # ranks of the in-kernel xGMI engine use the framework's device barrier (one xGMI
+    # hop, parallel/xgmi.py:DeviceBarrier) instead of an RCCL collective
+    dbar = None
+    if world > 1 and a.impl == "native" and getattr(runner, "comm", "") == "xgmi":
+        from distributed_training_pytorch_amd.parallel.xgmi import DeviceBarrier
+
+        dbar = DeviceBarrier(dev)
+
+    def barrier():
+        if dbar is not None:
+            dbar()
+            sync()
+        else:
+            dist_env.barrier()
+
     # warmup (untimed)
     train(a.warmup)
     sync()
-    dist_env.barrier()
+    barrier()
     sync()
     t0 = time.perf_counter()
     train(a.steps)
     sync()
-    dist_env.barrier()
+    barrier()
     t1 = time.perf_counter()
     elapsed = dist_env.allreduce_max(t1 - t0, dev)
     ms_per_step = 1e3 * elapsed / a.steps
@@ -121,10 +137,14 @@ def main():
     value = total_samples / elapsed
 
     final_loss = None
+    if dbar is not None:
+        dbar.check()  # raises if a barrier exchange timed out
     if a.impl == "native":
         runner.check_comm()  # raises if any in-kernel exchange of the run timed out
         final_loss = runner.losses(runner.t - 1, runner.t)[0].tolist()
-        runner.close()
+        runner.close()  # process-group barrier before the xGMI buffers are unmapped
+        if dbar is not None:
+            dbar.close()
     else:
         final_loss = list(runner.last)
         runner.close()

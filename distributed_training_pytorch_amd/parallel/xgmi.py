@@ -168,3 +168,56 @@ class XgmiAllReduce:
 
     def close(self):
         self.bufs.close()
+
+
+class DeviceBarrier:
+    """All-rank barrier queued on the GPU stream: a one-float one-shot xGMI
+    all-reduce (``csrc/xgmi_allreduce.hip``), i.e. one hop of xGMI latency instead
+    of an RCCL collective.
+
+    ``barrier()`` then ``torch.cuda.synchronize()`` returns only after every rank
+    has queued its barrier -- and so finished everything queued before it: the
+    same guarantee as ``dist.barrier`` + synchronize, at the cost of a kernel
+    launch and one exchange.  If the xGMI buffers cannot be set up on every rank,
+    every rank agrees (one 1-element all-reduce) and falls back to the
+    process-group barrier.
+    """
+
+    def __init__(self, device: torch.device, group=None):
+        from . import comm_util
+
+        self.group = group
+        self.device = device
+        self._ar = None
+        ok = True
+        try:
+            self._ar = XgmiAllReduce(1, device, group)
+        except Exception:  # IPC / peer access unavailable on this rank
+            ok = False
+        flag = torch.tensor([0.0 if ok else 1.0])
+        comm_util.all_reduce_(flag, group)
+        if flag.item() != 0.0 and self._ar is not None:
+            self._ar.close()
+            self._ar = None
+        self._tok = torch.zeros(1, dtype=torch.float32, device=device)
+
+    @property
+    def native(self) -> bool:
+        return self._ar is not None
+
+    def __call__(self):
+        if self._ar is None:
+            from . import comm_util
+
+            comm_util.barrier(self.group)
+        else:
+            self._ar.all_reduce_(self._tok)
+
+    def check(self):
+        if self._ar is not None:
+            self._ar.check()
+
+    def close(self):
+        if self._ar is not None:
+            self._ar.close()
+            self._ar = None

@@ -85,3 +85,29 @@ def test_torch_order_matches_distributed_sampler():
         s = DistributedSampler(ds, num_replicas=W, rank=r, shuffle=True, seed=4)
         s.set_epoch(e)
         assert list(iter(s)) == torch_distributed_indices(100, W, r, e, seed=4)
+
+
+def _barrier_fn(rank, world):
+    import time
+
+    import torch
+
+    from distributed_training_pytorch_amd.parallel.xgmi import DeviceBarrier
+
+    bar = DeviceBarrier(torch.device("cpu"))
+    if rank == 1:
+        time.sleep(0.3)  # the late rank: rank 0's barrier must wait for it
+    t0 = time.perf_counter()
+    bar()
+    waited = time.perf_counter() - t0
+    native = bar.native
+    bar.close()
+    return waited, native
+
+
+def test_device_barrier_falls_back_to_the_process_group():
+    """Without xGMI buffers (CPU ranks) every rank agrees on the process-group
+    barrier; it still synchronises the ranks."""
+    res = run_ranks(_barrier_fn, 2, ())
+    assert res[0][1] is False and res[1][1] is False
+    assert res[0][0] > 0.2  # rank 0 waited for the late rank
