@@ -1,31 +1,23 @@
-// Scalar-weight decomposition of the fused train step (v3): one lane per sample,
-// weights in SGPRs.
+// Weight layouts and per-layer building blocks of the fused train step
+// (mlp_train.hip, mlp_pipe.h): one lane per sample.
 //
-// Why: in the toy MLP every lane of a wave needs the SAME weights at the same
-// time.  Read from LDS, each broadcast ds_read_b128 still moves 64 x 16 B through
-// the LDS data path (4 LDS cycles per wave-instruction at 256 B/clk/CU): the
-// v2 kernel spent ~6k of its ~14k cycles per step on weight broadcasts
-// (rocprofv3: 194 LDS instructions per wave per step).  Weights are instead read
-// with s_load_dwordx16 from a small per-model workspace in global memory (it
-// stays in the scalar cache) and feed v_pk_fma_f32 directly as SGPR-pair
-// operands: no LDS traffic, no VGPRs, no shuffles for weights at all.
-//
-//   * forward block FW(l): W_l^T [in][pad2(out)] then bias [pad2(out)], so a pair
-//     of consecutive outputs (j, j+1) of one input i is one aligned SGPR pair ->
-//     z[j:j+1] += W^T[i][j:j+1] * h_i  is one v_pk_fma_f32;
-//   * backward block BW(l), l >= 1: W_l [out][pad2(in)] (the torch layout with rows
-//     padded to even), so  g[i:i+1] += W[j][i:i+1] * dz_j  is one v_pk_fma_f32;
-//   * pad entries are zero and are never written by the optimizer.
-// Freshness: the optimizer phase writes updated weights with vector stores,
-// drains them (vmcnt(0)), barriers, and the next step starts with
-// s_dcache_inv; the workspace pointer is laundered through an empty asm each
-// step so the compiler can neither hoist nor CSE the scalar loads across steps.
+//   * LDS forward block of layer l: W_l^T [in][pad4(out)] then bias [pad4(out)], so
+//     consecutive outputs (j, j+1) of one input i are adjacent and
+//     z[j:j+1] += W^T[i][j:j+1] * h_i is one v_pk_fma_f32 straight from a broadcast
+//     ds_read_b128;
+//   * LDS backward block of layer l >= 1: W_l [out][pad4(in)] (the torch layout,
+//     rows padded), so g[i:i+1] += W[j][i:i+1] * dz_j is one v_pk_fma_f32;
+//   * pad entries are zero and are never written by the optimizer;
+//   * the dW tiles: per-wave staging of (dz, h) columns and 16 MFMA K-steps per tile,
+//     the first and last layers packed into one tile when they fit.
+// The round-1 variant that streamed the forward weights through SGPRs (s_load from
+// a global workspace) measured slower than the LDS blocks and was removed in round 2
+// (docs/perf_notes.md, v3); the workspace size query (WS) stays as the shape check.
 #pragma once
 #include "mlp_core.h"
 
 namespace dtp {
 
-typedef __attribute__((address_space(4))) const float cfloat;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <class S>
@@ -99,130 +91,6 @@ DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos, int& pfl) {
       pfl = SC::lfb(l) + j;
       tpos = base + (ro + j) * 16 + co + I;  // bias column = constant-1 input
     }
-  });
-}
-
-// Scalar-cache protocol per step:
-//   * the scalar cache is shared by all waves of the CU (and its neighbour), so it
-//     is invalidated ONCE per step at a point where no wave can still fill it with
-//     old weights: after the dW-reduction barrier (every wave has finished this
-//     step's forward/backward loads) and before the optimizer's stores;
-//   * after the end-of-step barrier (stores drained with vmcnt(0) first),
-//     fresh_weights() refills it with one s_load_dword per 64-byte line, all in
-//     flight at once (one L2 latency per step instead of one per weight group,
-//     overlapped with the sample gather), and hands out a laundered pointer so no
-//     weight load is hoisted above the refill.  The touch loads rotate over 8
-//     dummy SGPRs that stay live (read-write operands) until the closing
-//     s_waitcnt, so no in-flight touch can land in a register the compiler reused.
-template <int LN, int N>
-DTP_DEV void touch_lines(uint32_t (&d)[8], unsigned long long v) {
-  if constexpr (LN < N) {
-    asm volatile("s_load_dword %0, %1, %2" : "+s"(d[LN & 7]) : "s"(v), "i"(LN * 64));
-    touch_lines<LN + 1, N>(d, v);
-  }
-}
-
-template <int NLINES>
-DTP_DEV cfloat* fresh_weights(const float* w) {
-  unsigned long long v = reinterpret_cast<unsigned long long>(w);
-  asm volatile("" : "+s"(v));
-  uint32_t d[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-  touch_lines<0, NLINES>(d, v);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(d[0]), "s"(d[1]), "s"(d[2]), "s"(d[3]), "s"(d[4]), "s"(d[5]), "s"(d[6]),
-               "s"(d[7]));
-  return reinterpret_cast<cfloat*>(v);
-}
-
-// Weight streaming discipline.  The compiler treats the workspace as constant
-// memory: left alone it hoists every weight load of the step to the top (hundreds
-// of SGPRs -> spills through v_writelane) and merges them into wide s_loads.
-// Each layer is therefore streamed in GROUPS of G rows of its block (G inputs of
-// W^T forward, G outputs of W backward; G*width <= 24 floats): each group is
-// loaded through its own laundered pointer copy one group AHEAD of its use and
-// groups are fenced with sched_barrier, so <= 2 groups (<= 48 SGPRs) are live.
-// Inside a group the FMAs run input-major: every output pair is an independent
-// accumulation chain (5 chains for width 10), so v_pk_fma_f32 issues back to back
-// with no dependency stalls.  SMEM returns out of order, so every group wait is
-// an lgkmcnt(0): what the prefetch hides is the load latency minus one group's
-// FMAs.
-template <int N>
-struct SVals {
-  float v[N];
-};
-
-// opaque copy of the workspace pointer: loads through different copies cannot be
-// merged into one wide s_load (SILoadStoreOptimizer) nor hoisted above the copy
-DTP_DEV cfloat* launder(cfloat* w) {
-  unsigned long long v = reinterpret_cast<unsigned long long>(w);
-  asm volatile("" : "+s"(v));
-  return reinterpret_cast<cfloat*>(v);
-}
-
-template <int ROWLEN>
-constexpr int group_rows(int rows) {
-  int g = 24 / ROWLEN;
-  g = g < 1 ? 1 : g;
-  return g > rows ? rows : g;
-}
-
-// acc[q] (pairs) += sum over rows r of the block of row_r[2q .. 2q+1] * s_r, rows
-// [0, R) of a row-major SGPR-streamed block with row length RL (even) at `off`
-template <int R, int RL, class GetS, class Between>
-DTP_DEV void stream_block(cfloat* wbase, int off, f32x2 (&acc)[RL / 2], GetS&& sval, Between&& between) {
-  constexpr int G = group_rows<RL>(R);
-  constexpr int NG = (R + G - 1) / G;
-  auto load = [&](auto GC) {
-    constexpr int g = decltype(GC)::value;
-    constexpr int r0 = g * G, nr = (R - r0) < G ? (R - r0) : G;
-    cfloat* w = launder(wbase);
-    SVals<G * RL> t;
-    static_for<0, nr * RL>([&](auto EC) { t.v[decltype(EC)::value] = w[off + r0 * RL + decltype(EC)::value]; });
-    return t;
-  };
-  SVals<G * RL> cur = load(std::integral_constant<int, 0>{});
-  static_for<0, NG>([&](auto GC) {
-    constexpr int g = decltype(GC)::value;
-    constexpr int r0 = g * G, nr = (R - r0) < G ? (R - r0) : G;
-    SVals<G * RL> nxt;
-    if constexpr (g + 1 < NG) nxt = load(std::integral_constant<int, g + 1>{});
-    __builtin_amdgcn_sched_barrier(0);
-    between(std::integral_constant<int, g>{}, std::integral_constant<int, NG>{});
-    static_for<0, nr>([&](auto RC) {
-      constexpr int r = decltype(RC)::value;
-      const float sv = sval(std::integral_constant<int, r0 + r>{});
-      static_for<0, RL / 2>([&](auto QC) {
-        constexpr int q = decltype(QC)::value;
-        acc[q] = __builtin_elementwise_fma(f32x2{cur.v[r * RL + 2 * q], cur.v[r * RL + 2 * q + 1]}, f32x2{sv, sv},
-                                           acc[q]);
-      });
-    });
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (g + 1 < NG) cur = nxt;
-  });
-}
-
-// forward of one sample (lane): h[l+1] = act(W_l h[l] + b_l)
-template <class S>
-DTP_DEV void scal_forward(cfloat* wbase, float (&h)[S::NL + 1][16], float slope) {
-  using SC = Scal<S>;
-  static_for<0, S::NL>([&](auto LC) {
-    constexpr int l = decltype(LC)::value;
-    constexpr int I = S::din(l), O = S::dout(l), OP = SC::pad2(O), NP = OP / 2;
-    f32x2 z[NP];
-    {
-      cfloat* w = launder(wbase);
-      static_for<0, NP>([&](auto QC) {
-        constexpr int q = decltype(QC)::value;
-        z[q] = f32x2{w[SC::fbo(l) + 2 * q], w[SC::fbo(l) + 2 * q + 1]};
-      });
-    }
-    stream_block<I, OP>(wbase, SC::fwo(l), z, [&](auto IC) { return h[l][decltype(IC)::value]; },
-                        [](auto, auto) {});
-    static_for<0, O>([&](auto JC) {
-      constexpr int j = decltype(JC)::value;
-      const float v = (j & 1) ? z[j / 2].y : z[j / 2].x;
-      h[l + 1][j] = S::act(l) ? leaky(v, slope) : v;
-    });
   });
 }
 

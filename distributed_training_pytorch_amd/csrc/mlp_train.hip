@@ -28,9 +28,6 @@ constexpr int kDataCache = 12288;
 // Adam bias-correction scalars of the next kAdamTab steps, formed cooperatively in
 // f64 (torch's host math) once per kAdamTab steps instead of per step
 constexpr int kAdamTab = 1024;
-#ifndef DTP_SCALAR_FWD
-#define DTP_SCALAR_FWD 0
-#endif
 #ifndef DTP_PIPE
 #define DTP_PIPE 1  // software-pipelined forward/backward (mlp_pipe.h); 0 = the v5 schedule
 #endif
@@ -75,7 +72,8 @@ struct SampleRegs {
   } while (0)
 
 // Fused train step(s), one workgroup (4 waves, one lane per sample) per model.
-// Weights live in SGPRs (mlp_scalar.h), activations in VGPRs, the dW reduction
+// Weights live in LDS blocks read into registers one layer ahead (mlp_pipe.h),
+// activations in VGPRs, the dW reduction
 // over the batch runs on MFMA through a per-wave LDS staging area, the optimizer
 // owns NPT parameters per thread in registers (params and moments).
 #ifndef DTP_TRAIN_WAVES_PER_EU
@@ -100,9 +98,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
   constexpr bool kUpdate = MODE != DTP_MODE_GRAD;
-  // forward weights: SGPR stream from the global workspace (mlp_scalar.h) or LDS blocks
-  constexpr bool kScalarFwd = DTP_SCALAR_FWD;
-  constexpr bool kPipe = DTP_PIPE && !DTP_SCALAR_FWD && S::NL >= 3;
+  constexpr bool kPipe = DTP_PIPE && S::NL >= 3;
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
@@ -114,7 +110,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   // and exchange counters, the dataset) is issued before the first wait, so a
   // launch pays ONE memory round trip before its first step, not three.
   float* __restrict__ gp = a.params + (size_t)model * P;
-  float* __restrict__ ws = a.wsp + (size_t)model * SC::WS;
   const SamplerCfg smp = a.smp;
   const bool cached = FAST || (a.cache_data && smp.n * (S::IN + ydim) <= kDataCache);
   int pf[NPT], pb[NPT], tp[NPT], pfl[NPT];
@@ -130,8 +125,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   }
   const int t0 = a.step[model];
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
-  if constexpr (kScalarFwd)
-    for (int e = tid; e < SC::WS; e += kBlock) ws[e] = 0.f;
   for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   if (cached) {
     for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
@@ -140,12 +133,10 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   const float* __restrict__ Xg = a.X;
   const float* __restrict__ Yg = a.Y;
   const int yoff = smp.n * S::IN;
-  if constexpr (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pad zeros before the scatter
   __syncthreads();  // weight blocks zeroed (pads stay 0) before the owners scatter into them
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     if (NPT * tid + k < P) {
-      if (kScalarFwd) ws[pf[k]] = pw[k];
       sm.wb[pfl[k]] = pw[k];
       if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
     }
@@ -218,12 +209,10 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   };
   if (kAdam) fill_adam(0);
   float* const stg_pack = &sm.stage[wave][0][0];
-  if constexpr (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // workspace weights in L2
   __syncthreads();  // scattered weight blocks and the Adam table visible to every wave
 
   for (int it = 0; it < a.n_steps; ++it) {
     DTP_STAMP(0);
-    cfloat* w = nullptr;
     const int t = t0 + it;
     const BatchPos bp = batch_at(epoch, bi);
     const int bsz = bp.size;
@@ -247,10 +236,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
         pb0.template load<0, FBlk<S, 0>::NR>(sm.wb);
         if (c0 == 0) DTP_STAMP(1);
         pipe_forward<S, 0, FAST>(sm.wb, pb0, h, slope, pbt, pbt2);
-      } else if constexpr (kScalarFwd) {
-        if (c0 == 0) w = fresh_weights<SC::NLINES>(ws);
-        if (c0 == 0) DTP_STAMP(1);
-        scal_forward<S>(w, h, slope);
       } else {
         if (c0 == 0) DTP_STAMP(1);
         lds_forward<S>(sm.wb, h, slope);
@@ -287,7 +272,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       }
       if (c0 == 0) DTP_STAMP(2);
 
-      // ---------------- backward: dX chain (VALU, SGPR weights) + dW tiles (MFMA, K = samples)
+      // ---------------- backward: dX chain (VALU, LDS weight blocks) + dW tiles (MFMA, K = samples)
       if constexpr (kPipe) {
         const PipeBwdCtx<S> pc{sm.wb, stg_pack, &sm.stage[wave][1][0], lane, slope, lpart};
         pipe_backward<S>(pc, pbt, pbt2, h, dz, acc);
@@ -348,9 +333,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     // this step's Adam scalars: requested now, consumed after the reduction
     float2 adam_sc = make_float2(0.f, 1.f);
     if constexpr (kAdam) adam_sc = sm.adam_tab[it % kAdamTab];
-    // no wave loads this step's weights any more: drop them from the scalar cache
-    // before the optimizer writes the new ones (mlp_scalar.h protocol)
-    if (kScalarFwd && wave == 0) __builtin_amdgcn_s_dcache_inv();
     DTP_STAMP(4);
 
     float g[NPT];
@@ -420,7 +402,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const bool own = NPT * tid + k < P;
-        if (kScalarFwd && own) ws[pf[k]] = pw[k];
         *(own ? &sm.wb[pfl[k]] : &sm.sink[0]) = pw[k];
         *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
       }
@@ -431,7 +412,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
     }
     DTP_STAMP(6);
-    if (kScalarFwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight stores reached L2 before the barrier
     __syncthreads();  // updated weights visible; reduction tiles consumed
     // the next kAdamTab steps' Adam scalars, once every kAdamTab steps at a step
     // boundary (every wave read this step's entry before the barrier above)
@@ -537,7 +517,6 @@ int validate_train(const DtpTrainArgs* a, int mode) {
     return set_err(-1, "bad sampler geometry");
   if (a->smp.mode == dtp::SAMPLER_EXPLICIT && !a->idx) return set_err(-1, "explicit sampler without indices");
   if (a->loss_log && a->loss_log_cap <= 0) return set_err(-1, "loss_log_cap must be positive");
-  if (!a->wsp) return set_err(-1, "the weight workspace (wsp) is required");
   if (!a->params || !a->X || !a->Y || !a->step) return set_err(-1, "params, X, Y and step are required");
   if (mode == DTP_MODE_GRAD && !a->grad_out) return set_err(-1, "MODE_GRAD needs grad_out");
   if (mode != DTP_MODE_GRAD && !a->opt_m) return set_err(-1, "optimizer modes need opt_m");
