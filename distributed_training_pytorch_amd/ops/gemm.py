@@ -2,7 +2,8 @@
 
 The toy model's 10-wide layers run inside the fused train-step kernel
 (``ops/mlp.py``); any wider MLP -- ``models/wide.py`` -- runs its Linear layers
-through this LDS-tiled MFMA GEMM instead of hipBLASLt:
+through this op: an LDS-tiled MFMA GEMM with the Linear epilogues fused (or, for the
+large bf16 problems, hipBLASLt plus one epilogue pass -- see below):
 
 * forward    ``h' = LeakyReLU(h W^T + b)``       bias + activation in the epilogue;
 * grad input ``dz' = (dz W) * LeakyReLU'(h)``    activation gradient in the epilogue;
@@ -14,10 +15,23 @@ Replaces the reference's cuBLAS ``addmm``/``mm`` + ATen ``leaky_relu(_backward)`
 / ``sum`` kernels (``toy_model_and_data.py:12-25``).
 On CPU tensors every function runs the PyTorch reference of the same math (the
 gloo test paths); on a GPU the HIP kernels are required.
+
+Backend for large bf16 problems (``DTP_GEMM_BACKEND`` / ``set_backend``):
+``blaslt`` (default) runs the GEMM on hipBLASLt (``torch.mm``/``addmm``, fp32
+output through ``out_dtype``) with the epilogue as one extra in-place elementwise
+pass; ``mfma`` always runs the kernels above; ``auto`` times both once per problem
+signature (scratch outputs, events) and keeps hipBLASLt only when it is at least
+``_TUNE_MARGIN`` faster.  Measured end to end (``profiles/wide_r2/``), hipBLASLt for
+every large layer GEMM is the fastest of the three on the 1024/2048/4096-wide MLPs
+(1.73 / 2.00 / 5.42 ms per step vs 1.89 / 2.90 / 6.39 all-MFMA); the isolated
+per-problem timings of ``auto`` under-predict that gain.  Calls that pin a kernel
+(``fast`` / ``splitk`` / ``force_big``), fp32 operands, ``alpha != 1``, K <= 16,
+N or M == 1 and problems under ``_TUNE_MIN_FLOP`` always run the MFMA kernels.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -25,6 +39,30 @@ from .. import _native as nat
 
 _DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16}
 _BM = 128
+_BACKENDS = ("auto", "mfma", "blaslt")
+_backend = os.environ.get("DTP_GEMM_BACKEND", "blaslt")
+if _backend not in _BACKENDS:
+    raise ValueError(f"DTP_GEMM_BACKEND={_backend!r}: expected one of {_BACKENDS}")
+_TUNE_MIN_FLOP = 4e9      # below this the fused kernel (no extra epilogue pass) is kept
+_TUNE_MARGIN = 0.95       # hipBLASLt + epilogue pass must be >= 5 % faster
+_tuned: dict[tuple, str] = {}
+
+
+def set_backend(name: str) -> None:
+    """``blaslt`` | ``mfma`` | ``auto`` for the large bf16 GEMMs (see module doc)."""
+    global _backend
+    if name not in _BACKENDS:
+        raise ValueError(f"gemm backend {name!r}: expected one of {_BACKENDS}")
+    _backend = name
+
+
+def get_backend() -> str:
+    return _backend
+
+
+def tuned_choices() -> dict:
+    """{problem signature: backend} decided so far by ``auto``."""
+    return dict(_tuned)
 
 
 def _ld(t: torch.Tensor, name: str) -> int:
@@ -89,7 +127,20 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
             r = r + out.float()
         out.copy_(r.to(out_dtype))
         return out
-    lib = nat.require(a.device)
+    lib = nat.require(a.device)  # loud on a GPU box without the extension, whichever backend runs
+    pinned = fast is not None or splitk is not None or force_big
+    if (not pinned and _backend != "mfma" and _blaslt_eligible(a, M, N, K, alpha)
+            and not (accumulate and (aux is not None or act))):  # the kernel adds old C after the activation
+        key = (M, N, K, trans_a, trans_b, out_dtype, bias is not None, aux is not None, act, accumulate)
+        if _backend == "blaslt" or _choose(key, a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate,
+                                           out_dtype) == "blaslt":
+            return _gemm_blaslt(a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate, out_dtype)
+    return _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, out, bias, aux, act, slope, accumulate, alpha,
+                        splitk, out_dtype, force_big, fast)
+
+
+def _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, out, bias, aux, act, slope, accumulate, alpha, splitk,
+                 out_dtype, force_big, fast):
     if splitk is None:
         splitk = _auto_splitk(M, N, K, a.dtype) if (out_dtype == torch.float32 and not act and aux is None) else 1
     if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
@@ -110,6 +161,70 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     args.fast = 0 if fast is None else (int(fast) if fast is not True and fast is not False else (1 if fast else -1))
     nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
     return out
+
+
+def _blaslt_eligible(a: torch.Tensor, M: int, N: int, K: int, alpha: float) -> bool:
+    return (a.dtype == torch.bfloat16 and alpha == 1.0 and K > 16 and min(M, N) > 1
+            and 2.0 * M * N * K >= _TUNE_MIN_FLOP)
+
+
+def _gemm_blaslt(a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate, out_dtype):
+    """The same contract as the fused kernel, GEMM on hipBLASLt, epilogue in place after it."""
+    A = a.t() if trans_a else a        # [M, K]
+    Bt = b if trans_b else b.t()       # [K, N]
+    lowp = out_dtype == a.dtype
+    if accumulate:
+        if lowp:
+            out.add_(torch.mm(A, Bt))
+        else:
+            torch.addmm(out, A, Bt, out_dtype=out_dtype, out=out)
+        if bias is not None:
+            out.add_(bias)
+    elif bias is not None:
+        if lowp:
+            torch.addmm(bias.to(out_dtype), A, Bt, out=out)
+        else:
+            torch.addmm(bias.float(), A, Bt, out_dtype=out_dtype, out=out)
+    elif lowp:
+        torch.mm(A, Bt, out=out)
+    else:
+        torch.mm(A, Bt, out_dtype=out_dtype, out=out)
+    if aux is not None:  # out *= LeakyReLU'(aux), one pass, in place
+        aux = aux if aux.dtype == out.dtype else aux.to(out.dtype)
+        torch.ops.aten.leaky_relu_backward.grad_input(out, aux, slope, False, grad_input=out)
+    if act:
+        torch.nn.functional.leaky_relu_(out, slope)
+    return out
+
+
+def _event_ms(fn, reps: int = 8) -> float:
+    fn()  # first call: hipBLASLt heuristic lookup / code object load
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _choose(key, a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate, out_dtype) -> str:
+    got = _tuned.get(key)
+    if got is not None:
+        return got
+    if torch.cuda.is_current_stream_capturing():
+        return "mfma"  # no timing inside a graph capture; decided on the next eager call
+    scratch = out.clone()  # the caller's output is never written by the trial runs
+    lib = nat.require(a.device)
+    M, N = out.shape
+    K = a.shape[0] if trans_a else a.shape[1]
+    t_mfma = _event_ms(lambda: _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, scratch, bias, aux, act, slope,
+                                            accumulate, 1.0, None, out_dtype, False, None))
+    t_lt = _event_ms(lambda: _gemm_blaslt(a, b, trans_a, trans_b, scratch, bias, aux, act, slope, accumulate,
+                                          out_dtype))
+    del scratch
+    _tuned[key] = "blaslt" if t_lt < _TUNE_MARGIN * t_mfma else "mfma"
+    return _tuned[key]
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
@@ -159,7 +274,7 @@ def _grad_ready(p: torch.Tensor) -> None:
 
 
 class MLPFunction(torch.autograd.Function):
-    """y = L_{n-1}(... LeakyReLU(L_0(x)) ...) with every matmul on the MFMA GEMM.
+    """y = L_{n-1}(... LeakyReLU(L_0(x)) ...) with every matmul through ``gemm``.
 
     ``compute_dtype`` bf16 = autocast-style mixed precision: fp32 master weights
     cast once per forward, bf16 activations, fp32 accumulation and fp32 weight /

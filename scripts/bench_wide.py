@@ -93,7 +93,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--impl", choices=["ours", "stock", "both"], default="both")
+    ap.add_argument("--gemm-backend", choices=["auto", "mfma", "blaslt"], default=None,
+                    help="ops/gemm.py backend for our implementation (default: DTP_GEMM_BACKEND or auto)")
     a = ap.parse_args()
+    from distributed_training_pytorch_amd.ops import gemm as gemm_mod
+
+    if a.gemm_backend:
+        gemm_mod.set_backend(a.gemm_backend)
     rank, world, local = dist_env.init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -116,7 +122,12 @@ def main():
             print(json.dumps({"impl": impl, "width": a.width, "depth": a.depth, "batch_per_rank": a.batch,
                               "world": world, "ms_per_step": 1e3 * dt / a.steps,
                               "samples_per_s": a.batch * world * a.steps / dt, "model_tflops": flops / dt / 1e12,
-                              "dtype": "bf16 compute, fp32 master weights"}), flush=True)
+                              "dtype": "bf16 compute, fp32 master weights",
+                              "gemm_backend": gemm_mod.get_backend() if impl == "ours" else "torch",
+                              "tuned": {"x".join(map(str, k[:3])) + ("T" if k[3] else "N") + ("T" if k[4] else "N")
+                                        + ("+acc" if k[9] else "") + ("+aux" if k[7] else "") + ("+act" if k[8] else ""):
+                                        v for k, v in gemm_mod.tuned_choices().items()} if impl == "ours" else {}}),
+                  flush=True)
         del step
         torch.cuda.empty_cache()
     if dist.is_initialized():

@@ -70,3 +70,20 @@ def test_wide_mlp_fused_grad_accumulates_in_place():
     for _ in range(2):
         torch.nn.functional.mse_loss(ref.reference_forward(x), y).backward()
     torch.testing.assert_close(got, torch.cat([p.grad.reshape(-1) for p in ref.parameters()]), rtol=1e-5, atol=1e-6)
+
+
+def test_gemm_backend_knob():
+    from distributed_training_pytorch_amd.ops import gemm as g
+
+    prev = g.get_backend()
+    try:
+        for name in ("mfma", "blaslt", "auto"):
+            g.set_backend(name)
+            assert g.get_backend() == name
+        with pytest.raises(ValueError):
+            g.set_backend("cublas")
+    finally:
+        g.set_backend(prev)
+    # on CPU tensors every backend runs the PyTorch reference
+    a, b = torch.randn(64, 32).bfloat16(), torch.randn(48, 32).bfloat16()
+    torch.testing.assert_close(g.gemm(a, b, out_dtype=torch.float32), a.float() @ b.float().t())
