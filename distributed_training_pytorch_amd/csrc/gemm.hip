@@ -899,8 +899,10 @@ int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
 // running a 128x128 MFMA tile with 1/16th of its K used.  Block = kSkinnyRows rows x
 // 256 columns (the B block staged once per 128 rows, not per 16); thread t owns
 // columns 8 (t & 31) .. +8 of rows 2 (t >> 5) + 16 q .. +2, q < kSkinnyRows / 16.
+// KC = K at compile time (1, 2: the usual MLP in/out widths; 0 = K read at run time):
+// the thread's 8 B columns then live in registers for all of its rows.
 constexpr int kSkinnyRows = 128;
-template <int DT, bool TA, bool TB>
+template <int DT, bool TA, bool TB, int KC = 0>
 __global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
   __shared__ float sa[kSkinnyRows][17];
   __shared__ float sb[256][17];
@@ -929,6 +931,13 @@ __global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
   char* C = static_cast<char*>(a.C);
   const char* aux = static_cast<const char*>(a.aux);
   const bool vec_c = (a.ldc % 8 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) && n0 + cc + 8 <= a.N;
+  float breg[8][KC > 0 ? KC : 1];
+  if constexpr (KC > 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) breg[c][k] = sb[cc + c][k];
+  }
   for (int rq = 0; rq < kSkinnyRows * 2 / 16; ++rq) {
     const int r = rq & 1, lr = rr + r + 16 * (rq >> 1);
     const int m = m0 + lr;
@@ -937,7 +946,12 @@ __global__ __launch_bounds__(256) void gemm_skinny_k_kernel(DtpGemmArgs a) {
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float t = 0.f;
-      for (int k = 0; k < a.K; ++k) t = fmaf(sa[lr][k], sb[cc + c][k], t);
+      if constexpr (KC > 0) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) t = fmaf(sa[lr][k], breg[c][k], t);
+      } else {
+        for (int k = 0; k < a.K; ++k) t = fmaf(sa[lr][k], sb[cc + c][k], t);
+      }
       acc[c] = t;
       v[c] = a.alpha * t + bias[c];
     }
@@ -1055,6 +1069,72 @@ __global__ __launch_bounds__(256) void colsum_bf16x8_kernel(const void* X, long 
   }
 }
 
+
+// Skinny-output weight gradient (an MLP's first Linear, dW [out, in <= 4], or its last,
+// dW [out <= 4, in]): C (+)= alpha A^T B with both operands K-major ([K, M], [K, N]) and
+// min(M, N) <= 4 -- the wide operand's column sums weighted by the J skinny columns.
+// Pure read bandwidth of the wide operand: a thread owns 8 adjacent wide columns
+// (16-byte loads, 4 rows in flight), 8 row groups x 32 rows per block, row blocks meet
+// in f32 atomics.  out[w * so + j * sj] for wide index w and skinny index j.
+constexpr int kSkinnyOutRows = 256;
+template <int J>
+__global__ __launch_bounds__(256) void gemm_skinny_out_kernel(const uint16_t* X, long long ldx, const uint16_t* Y,
+                                                              long long ldy, int K, int W, float* out, long long so,
+                                                              long long sj, float alpha) {
+  __shared__ float red[8][256 * J];
+  const int cc = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int w0 = blockIdx.x * 256 + cc * 8;
+  const int r0 = blockIdx.y * kSkinnyOutRows;
+  const int r1 = min(K, r0 + kSkinnyOutRows);
+  float s[J][8];
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[j][e] = 0.f;
+  auto add = [&](const uint4& v, int m) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[2 * e] = __uint_as_float(w[e] << 16);
+      x[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const float y = bf16_to_f32(Y[static_cast<long long>(m) * ldy + j]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[j][e] = fmaf(x[e], y, s[j][e]);
+    }
+  };
+  if (w0 < W) {
+    const uint16_t* base = X + w0;
+    int m = r0 + g;
+    for (; m + 24 < r1; m += 32) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(base + static_cast<long long>(m + 8 * u) * ldx);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u], m + 8 * u);
+    }
+    for (; m < r1; m += 8) add(*reinterpret_cast<const uint4*>(base + static_cast<long long>(m) * ldx), m);
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[g][j * 256 + cc * 8 + e] = s[j][e];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = threadIdx.x, w = blockIdx.x * 256 + c;
+    if (w < W) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += red[q][j * 256 + c];
+      atomicAdd(out + static_cast<long long>(w) * so + static_cast<long long>(j) * sj, alpha * t);
+    }
+  }
+}
+
 }  // namespace gemm
 }  // namespace dtp
 
@@ -1069,6 +1149,35 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   if (a.dtype != DTP_DT_F32 && a.dtype != DTP_DT_BF16) return set_err(1, "dtp_gemm: dtype must be f32 or bf16");
   if (a.out_dtype != DTP_DT_F32 && a.out_dtype != DTP_DT_BF16) return set_err(1, "dtp_gemm: bad out dtype");
   if (!a.A || !a.B || !a.C) return set_err(1, "dtp_gemm: null operand");
+  // skinny-output weight gradient: bandwidth kernel over the wide operand (any split-K
+  // request is moot: every row block already meets in atomics)
+  if (a.dtype == DTP_DT_BF16 && a.trans_a && a.trans_b && a.out_dtype == DTP_DT_F32 && !a.act && !a.aux &&
+      !a.bias && (a.M <= 4 || a.N <= 4) && a.K >= 64) {
+    const bool wide_a = a.N <= 4;  // dW [out, in <= 4]: A = dz is the wide operand
+    const void* X = wide_a ? a.A : a.B;
+    const void* Y = wide_a ? a.B : a.A;
+    const long long ldx = wide_a ? a.lda : a.ldb, ldy = wide_a ? a.ldb : a.lda;
+    const int W = wide_a ? a.M : a.N, J = wide_a ? a.N : a.M;
+    if (W % 8 == 0 && ldx % 8 == 0 && aligned16(X)) {
+      hipStream_t s = static_cast<hipStream_t>(stream);
+      if (!a.accumulate) {
+        hipError_t e = hipMemset2DAsync(a.C, sizeof(float) * static_cast<size_t>(a.ldc), 0, sizeof(float) * a.N, a.M, s);
+        if (e != hipSuccess) return set_err(2, "dtp_gemm: clearing the skinny-output C failed");
+      }
+      const long long so = wide_a ? a.ldc : 1, sj = wide_a ? 1 : a.ldc;
+      const dim3 g((W + 255) / 256, (a.K + gemm::kSkinnyOutRows - 1) / gemm::kSkinnyOutRows), b(256);
+      const auto* Xh = static_cast<const uint16_t*>(X);
+      const auto* Yh = static_cast<const uint16_t*>(Y);
+      float* C = static_cast<float*>(a.C);
+      switch (J) {
+        case 1: hipLaunchKernelGGL(gemm::gemm_skinny_out_kernel<1>, g, b, 0, s, Xh, ldx, Yh, ldy, a.K, W, C, so, sj, a.alpha); break;
+        case 2: hipLaunchKernelGGL(gemm::gemm_skinny_out_kernel<2>, g, b, 0, s, Xh, ldx, Yh, ldy, a.K, W, C, so, sj, a.alpha); break;
+        case 3: hipLaunchKernelGGL(gemm::gemm_skinny_out_kernel<3>, g, b, 0, s, Xh, ldx, Yh, ldy, a.K, W, C, so, sj, a.alpha); break;
+        default: hipLaunchKernelGGL(gemm::gemm_skinny_out_kernel<4>, g, b, 0, s, Xh, ldx, Yh, ldy, a.K, W, C, so, sj, a.alpha); break;
+      }
+      return check_launch("dtp_gemm(skinny output)");
+    }
+  }
   if (a.splitk < 1) a.splitk = 1;
   if (a.splitk > 1 && (a.out_dtype != DTP_DT_F32 || a.act || a.aux))
     return set_err(1, "dtp_gemm: split-K needs an f32 output and no activation epilogue");
@@ -1093,8 +1202,16 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
       case 1: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, false, true>), gs, bs, 0, s, a); break;
       case 2: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, true, false>), gs, bs, 0, s, a); break;
       case 3: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_F32, true, true>), gs, bs, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, false>), gs, bs, 0, s, a); break;
-      case 5: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, true>), gs, bs, 0, s, a); break;
+      case 4:
+        if (a.K == 2) hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, false, 2>), gs, bs, 0, s, a);
+        else if (a.K == 1) hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, false, 1>), gs, bs, 0, s, a);
+        else hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, false>), gs, bs, 0, s, a);
+        break;
+      case 5:
+        if (a.K == 1) hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, true, 1>), gs, bs, 0, s, a);
+        else if (a.K == 2) hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, true, 2>), gs, bs, 0, s, a);
+        else hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, false, true>), gs, bs, 0, s, a);
+        break;
       case 6: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, true, false>), gs, bs, 0, s, a); break;
       default: hipLaunchKernelGGL((gemm::gemm_skinny_k_kernel<DTP_DT_BF16, true, true>), gs, bs, 0, s, a); break;
     }

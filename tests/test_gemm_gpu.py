@@ -4,10 +4,21 @@ import pytest
 import torch
 
 from distributed_training_pytorch_amd.models.wide import WideMLP
+from distributed_training_pytorch_amd.ops import gemm as gemm_mod
 from distributed_training_pytorch_amd.ops.gemm import colsum, gemm
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _mfma_backend(request):
+    """These tests check the HIP kernels: no large problem may be handed to hipBLASLt
+    unless the test asks for a backend itself."""
+    prev = gemm_mod.get_backend()
+    gemm_mod.set_backend(getattr(request, "param", "mfma"))
+    yield
+    gemm_mod.set_backend(prev)
 
 
 def _ref(a, b, ta, tb):
@@ -227,3 +238,56 @@ def test_toy_model_wide_width_runs_on_gemm_path():
     torch.nn.functional.mse_loss(m.layers(x), y).backward()
     for g, p in zip(got, m.parameters()):
         torch.testing.assert_close(g, p.grad, rtol=1e-4, atol=1e-5)
+
+
+def _wide_layer_cases(Bsz, W, slope=0.01):
+    """The wide MLP's hidden-layer GEMMs with their epilogues: (kwargs, a, b, fp32 reference)."""
+    g = torch.Generator().manual_seed(21)
+    h = (torch.rand(Bsz, W, generator=g) * 2 - 1).to(DEV, torch.bfloat16)
+    w = ((torch.rand(W, W, generator=g) * 2 - 1) / W ** 0.5).to(DEV, torch.bfloat16)
+    dz = (torch.rand(Bsz, W, generator=g) * 2 - 1).to(DEV, torch.bfloat16)
+    bias = torch.rand(W, generator=g).to(DEV) - 0.5
+    old = torch.randn(W, W, generator=g).to(DEV)
+    hf, wf, dzf = h.float(), w.float(), dz.float()
+    return [
+        ("fwd", dict(a=h, b=w, bias=bias, act=True, slope=slope, out_dtype=torch.bfloat16),
+         torch.nn.functional.leaky_relu(hf @ wf.t() + bias, slope), 2e-2),
+        ("last", dict(a=h, b=w, bias=bias, out_dtype=torch.float32), hf @ wf.t() + bias, 1e-3),
+        ("dx", dict(a=dz, b=w, trans_b=True, aux=h, slope=slope, out_dtype=torch.bfloat16),
+         (dzf @ wf) * torch.where(hf > 0, 1.0, slope), 2e-2),
+        ("dx0", dict(a=dz, b=w, trans_b=True, out_dtype=torch.float32), dzf @ wf, 1e-3),
+        ("dW", dict(a=dz, b=h, trans_a=True, trans_b=True, out=old.clone(), accumulate=True),
+         dzf.t() @ hf + old, 1e-3),
+    ]
+
+
+@pytest.mark.parametrize("backend", ["blaslt", "auto"])
+def test_gemm_backends_on_wide_layers(backend):
+    """hipBLASLt + epilogue pass (and the timed auto choice) give the fused kernel's results
+    on the wide-MLP layer problems; auto records one decision per problem signature."""
+    gemm_mod.set_backend(backend)
+    gemm_mod._tuned.clear()
+    for name, kw, ref, tol in _wide_layer_cases(2048, 1024):
+        a, b = kw.pop("a"), kw.pop("b")
+        got = gemm(a, b, **kw)
+        rel = (got.float() - ref).abs().max() / ref.abs().max()
+        assert rel < tol, (name, rel.item())
+    if backend == "auto":
+        assert len(gemm_mod.tuned_choices()) == 5
+        assert set(gemm_mod.tuned_choices().values()) <= {"mfma", "blaslt"}
+    gemm_mod.set_backend("mfma")
+    gemm_mod._tuned.clear()
+
+
+@pytest.mark.parametrize("M,N", [(1032, 2), (1, 1032), (3, 520), (2048, 4)])
+@pytest.mark.parametrize("K", [300, 8200])
+def test_gemm_skinny_output_weight_grad(M, N, K):
+    """dW of an MLP's first / last Linear (min(M, N) <= 4, both operands K-major): the
+    bandwidth kernel over the wide operand, fresh output, accumulate, alpha."""
+    a, b = _ops(M, N, K, True, True, torch.bfloat16, 17)
+    ref = _ref(a, b, True, True)
+    c = gemm(a, b, trans_a=True, trans_b=True, out_dtype=torch.float32)
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+    old = torch.randn(M, N, device=DEV)
+    c = gemm(a, b, trans_a=True, trans_b=True, out=old.clone(), accumulate=True, alpha=0.5)
+    torch.testing.assert_close(c, 0.5 * ref + old, rtol=1e-4, atol=1e-3 * K ** 0.5)
