@@ -285,9 +285,9 @@ class FusedTrainer:
                 if remaining >= G:
                     self._graph_launch(G)
                     k = G
-                else:
+                else:  # a tail shorter than the captured graph: one-step launches via the native executor
                     k = 1
-                    self._launch(1)
+                    self._run_engine(1)
             else:
                 k = 1
                 self._run_engine(1)

@@ -19,7 +19,7 @@ run() {  # name secs args...
   return $rc
 }
 run persistent 240 --steps 2000 --warmup 200 &&
-run graph 240 --steps 500 --warmup 50 --launch graph &&
+run graph 240 --steps 500 --warmup 50 --launch graph --steps-per-launch 50 &&
 run eager 240 --steps 300 --warmup 30 --launch eager &&
 run stock 300 --steps 200 --warmup 20 --impl stock &&
 timeout -k 10 60 rocprofv3 -L > "$out/counters.txt" 2>&1

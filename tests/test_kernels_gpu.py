@@ -112,7 +112,7 @@ def test_fused_trainer_matches_reference(launch):
     cfg = OptimConfig(lr=1e-2)
     tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, cfg,
                       EngineConfig(launch=launch, steps_per_launch=4), init_params=init)
-    steps = 12
+    steps = 14  # graph: three 4-step graphs, then a 2-step tail of one-step launches
     tr.train(steps)
     tr.synchronize()
     ref_p, ref_l = _ref_train(TOY_SPEC, torch.stack(init), X, Y, geom, steps, cfg)
