@@ -192,6 +192,10 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
             tr.synchronize()
             checkpoint.save({**tr.state_dict(), "engine": "fused", "config": vars(config)},
                             config.checkpoint_dir, it)
+            # the other ranks wait for rank 0's write on the host (process-group
+            # timeout), not inside the next launch's first in-kernel xGMI exchange,
+            # whose bounded spin a slow checkpoint filesystem could outlast
+            comm_util.barrier()
     tr.synchronize()
     dt = time.perf_counter() - t0
     if pbar is not None:
