@@ -20,15 +20,14 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402
 
 from argument_parser import build_parser  # noqa: E402
-from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry  # noqa: E402
+from distributed_training_pytorch_amd.data.sampler import BatchIndexer, SamplerGeometry  # noqa: E402
 from distributed_training_pytorch_amd.data.toy_data import ToyData  # noqa: E402
 from distributed_training_pytorch_amd.engine import runner  # noqa: E402
 from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
 from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig  # noqa: E402
-from distributed_training_pytorch_amd.parallel import comm_util  # noqa: E402
 from distributed_training_pytorch_amd.parallel.layer_split import LayerSplitDDP, LayerSplitMLP  # noqa: E402
 from distributed_training_pytorch_amd.runtime.errors import FaultInjector, check_replicas, record  # noqa: E402
-from distributed_training_pytorch_amd.utils.logging import MetricLogger, rank_print  # noqa: E402
+from distributed_training_pytorch_amd.utils.logging import LossRing, MetricLogger, rank_print  # noqa: E402
 
 
 def get_args(argv=None):
@@ -80,19 +79,29 @@ def main(argv=None):
     Yl = Y.to(devs[-1])
     geom = SamplerGeometry(n=config.n_samples, world=world, rank=rank, batch=config.batch_size,
                            distributed=config.dataloader == "distributed", seed=0)
-    idx_stream = EpochIndexStream(geom) if config.sampler == "torch" else None
+    indexer = BatchIndexer(geom, devs[0], exact_torch=config.sampler == "torch")
     logger = MetricLogger(project=config.project, group="multi-gpu-per-node", log_dir=config.log_dir, rank=rank)
     faults = FaultInjector(config.fail_at_iter, config.fail_rank, rank)
     lossf = torch.nn.MSELoss()
     pbar = runner._progress(rank, config.iters, config)
-    lbuf = torch.zeros(1, device=devs[-1])
+    # losses stay on the last stage's GPU; reduced and logged once per log_every steps
+    ring = LossRing(max(1, config.log_every), 1, devs[-1], world)
+    last = float("nan")
+
+    def flush():
+        nonlocal last
+        for step, (v,) in ring.flush():
+            if rank == 0:
+                # the reference logs the local loss (demo_one_model_multi_gpu.py:129-130); this is the global mean
+                logger.log({"loss/loss": v}, step=step)
+            last = v
+
     t0 = time.perf_counter()
     for it in range(config.iters):
         faults.check(it)
-        idx = idx_stream.indices(it) if idx_stream is not None else geom.indices(it)
-        i0 = torch.tensor(idx, device=devs[0])
-        x = X[i0]
-        y = Yl[i0.to(devs[-1])]
+        i0 = indexer(it)
+        x = X.index_select(0, i0)
+        y = Yl.index_select(0, i0.to(devs[-1]))
         model.zero_grad()
         out = model(x)
         loss = lossf(out, y)
@@ -100,13 +109,12 @@ def main(argv=None):
         ddp.allreduce_grads()
         for o in opts:
             o.step()
-        lbuf.copy_(loss.detach().reshape(1))
-        comm_util.all_reduce_(lbuf)
-        if rank == 0:
-            # the reference logs the local loss (demo_one_model_multi_gpu.py:129-130); this is the global mean
-            logger.log({"loss/loss": lbuf.item() / world}, step=it)
+        ring.put(it, loss)
+        if ring.full():
+            flush()
         if pbar is not None:
             pbar.update(1)
+    flush()
     for d in set(devs):
         if d.type == "cuda":
             torch.cuda.synchronize(d)
@@ -116,7 +124,7 @@ def main(argv=None):
     if config.check_replicas:
         check_replicas(model.flat_params_cpu())
     logger.finish()
-    summary = {"final_loss": lbuf.item() / world, "iters": config.iters, "stages": len(devs),
+    summary = {"final_loss": last, "iters": config.iters, "stages": len(devs),
                "microbatches": config.microbatches,
                "samples_per_s": geom.batch * config.iters * world / max(dt, 1e-9)}
     rank_print(rank, "Finished")

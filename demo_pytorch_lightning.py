@@ -84,8 +84,11 @@ def main(argv=None):
                          default_root_dir=a.root_dir, enable_progress_bar=not a.no_progress, seed=a.seed)
     trainer.fit(model, dl)
     if getattr(trainer, "global_rank", 0) == 0:
+        sps = None
+        if getattr(trainer, "fit_time", None):
+            sps = trainer.global_step * a.batch_size * getattr(trainer, "world_size", 1) / trainer.fit_time
         print(f"[Process 0] summary: {{'global_step': {trainer.global_step}, 'metrics': {trainer.callback_metrics}, "
-              f"'checkpoint': {trainer.checkpoint_path!r}}}", flush=True)
+              f"'checkpoint': {trainer.checkpoint_path!r}, 'samples_per_s': {sps}}}", flush=True)
     if hasattr(trainer, "teardown"):
         trainer.teardown()
 

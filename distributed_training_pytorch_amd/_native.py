@@ -98,6 +98,7 @@ class StageArgs(ctypes.Structure):
         ("out_peer", c_void_p),
         ("batch", c_int),
         ("slope", c_float),
+        ("accumulate", c_int),
     ]
 
 

@@ -64,11 +64,12 @@ struct DtpStageArgs {
   float* saved;           // [B][(NL-1)*H] hidden activations
   const float* grad_out;  // [B][OUT]  (backward)
   float* grad_in;         // [B][IN]   (backward, nullable)
-  float* grad_params;     // [P]       (backward; must be zeroed when the grid has >1 block)
+  float* grad_params;     // [P]       (backward; must be zeroed when the grid has >1 block and !accumulate)
   float* out_peer;        // [B][OUT]  forward: second copy of the output stored straight into
                           //           the next stage's GPU (peer-mapped over xGMI), nullable
   int batch;
   float slope;
+  int accumulate;  // backward: add into grad_params (a persistent .grad view) instead of overwriting it
 };
 
 int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
   for (int p = tid; p < S::P; p += kBlock) {
     const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
     if (gridDim.x == 1)
-      a.grad_params[p] = g;
+      a.grad_params[p] = a.accumulate ? a.grad_params[p] + g : g;
     else
       atomicAdd(&a.grad_params[p], g);
   }
@@ -137,7 +137,7 @@ template <class S>
 int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
   if (a->batch <= 0) return 0;
   // one block reduces deterministically up to 4 chunks; larger batches spread
-  // over more CUs and combine with float atomics into the zeroed grad buffer
+  // over more CUs and combine with float atomics into the zeroed (or accumulated) grad buffer
   int nblk = (a->batch + 4 * dtp::kBlock - 1) / (4 * dtp::kBlock);
   if (nblk > 256) nblk = 256;
   dim3 grid(nblk), block(dtp::kBlock);

@@ -16,8 +16,9 @@ as the reference uses them (``demo.py:139-154``):
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 M32 = 0xFFFFFFFF
@@ -61,6 +62,35 @@ def feistel_permute(q: int, n: int, bits: int, keys: list[int]) -> int:
             return q
 
 
+def _hash32_np(x: np.ndarray) -> np.ndarray:
+    """hash32 over a uint32 array (numpy uint32 products wrap mod 2**32, like the device)."""
+    x = x ^ (x >> 16)
+    x = x * np.uint32(0x7FEB352D)
+    x = x ^ (x >> 15)
+    x = x * np.uint32(0x846CA68B)
+    return x ^ (x >> 16)
+
+
+def feistel_permute_array(q: np.ndarray, n: int, bits: int, keys: list[int]) -> np.ndarray:
+    """:func:`feistel_permute` of every element of ``q`` at once (same cycle walk)."""
+    r = bits >> 1 if bits > 1 else 1
+    rmask = np.uint32((1 << r) - 1)
+    dmask = np.uint32((1 << bits) - 1)
+    ks = [np.uint32(k & M32) for k in keys]
+    cur = np.asarray(q, dtype=np.uint32)
+    out = np.empty(cur.shape, dtype=np.int64)
+    todo = np.arange(cur.size)
+    while todo.size:
+        for i in range(4):
+            hi = cur >> np.uint32(r)
+            lo = (cur & rmask) ^ (_hash32_np(hi ^ ks[i]) & rmask)
+            cur = ((lo << np.uint32(bits - r)) | hi) & dmask
+        ok = cur < n
+        out[todo[ok]] = cur[ok]
+        todo, cur = todo[~ok], cur[~ok]
+    return out
+
+
 def bits_for(n: int) -> int:
     return max(1, math.ceil(math.log2(max(n, 2))))
 
@@ -76,6 +106,7 @@ class SamplerGeometry:
     shuffle: bool = True
     distributed: bool = True
     seed: int = 0
+    _epoch_cache: tuple = field(default=(-1, None), init=False, repr=False, compare=False)
 
     @property
     def mode(self) -> int:
@@ -105,17 +136,25 @@ class SamplerGeometry:
     def batch_size_at(self, t: int) -> int:
         return self.batch_pos(t)[2]
 
+    def epoch_indices(self, epoch: int) -> np.ndarray:
+        """This rank's whole epoch in device-sampler order (int64 array of num_samples),
+        computed vectorised once per epoch (the last epoch is cached)."""
+        if self._epoch_cache[0] == epoch:
+            return self._epoch_cache[1]
+        j = np.arange(self.num_samples, dtype=np.int64)
+        if self.mode == SAMPLER_SEQUENTIAL:
+            idx = j
+        else:
+            q = (self.rank + j * self.world) % self.n  # padded list (padding repeats from the start)
+            idx = feistel_permute_array(q, self.n, self.bits, epoch_keys(self.seed, epoch)) \
+                if self.mode == SAMPLER_DIST_SHUFFLE else q
+        self._epoch_cache = (epoch, idx)
+        return idx
+
     def indices(self, t: int) -> list[int]:
         """Dataset indices of global step t on this rank (device-sampler order)."""
         epoch, start, size = self.batch_pos(t)
-        if self.mode == SAMPLER_SEQUENTIAL:
-            return list(range(start, start + size))
-        keys = epoch_keys(self.seed, epoch)
-        out = []
-        for k in range(size):
-            q = (self.rank + (start + k) * self.world) % self.n
-            out.append(feistel_permute(q, self.n, self.bits, keys) if self.mode == SAMPLER_DIST_SHUFFLE else q)
-        return out
+        return self.epoch_indices(epoch)[start:start + size].tolist()
 
     def to_native(self):
         from .._native import SamplerCfg
@@ -150,8 +189,7 @@ class EpochIndexStream:
         self._epoch = -1
         self._idx: list[int] = []
 
-    def indices(self, t: int) -> list[int]:
-        epoch, start, size = self.geom.batch_pos(t)
+    def epoch_list(self, epoch: int) -> list[int]:
         if epoch != self._epoch:
             g = self.geom
             if g.distributed:
@@ -159,4 +197,65 @@ class EpochIndexStream:
             else:
                 self._idx = list(range(g.n))
             self._epoch = epoch
-        return self._idx[start:start + size]
+        return self._idx
+
+    def indices(self, t: int) -> list[int]:
+        epoch, start, size = self.geom.batch_pos(t)
+        return self.epoch_list(epoch)[start:start + size]
+
+
+class BatchIndexer:
+    """Per-step batch indices as a tensor on ``device``, for the engines that gather
+    batches with ``index_select`` (module engine, layer split).
+
+    * device sampler on a GPU: ``block`` steps of indices at a time straight into a
+      device buffer by the native sampler kernel (``csrc/sampler.h``,
+      ``dtp_sampler_indices``): no host index math and no host-to-device copy per
+      step, stream-ordered with the steps that read them;
+    * exact torch order (``exact_torch``) or CPU: one vectorised epoch on the host,
+      uploaded once per epoch (pinned, asynchronous).
+    A returned tensor is a view that stays valid until ``block`` steps later.
+    """
+
+    def __init__(self, geom: SamplerGeometry, device: torch.device, exact_torch: bool = False, block: int = 64):
+        self.geom = geom
+        self.device = torch.device(device)
+        self.exact = exact_torch
+        self.block = max(1, int(block))
+        self._native = None
+        self._b0 = None
+        self._buf = None
+        self._epoch = -1
+        self._ep_idx = None
+        self._stream = EpochIndexStream(geom) if exact_torch else None
+        if self.device.type == "cuda" and not exact_torch:
+            from .. import _native as nat
+
+            if nat.native_enabled():
+                self._native = nat.require(self.device)
+                self._cfg = geom.to_native()
+                self._buf = torch.empty(self.block, geom.batch, dtype=torch.int32, device=self.device)
+
+    def __call__(self, t: int) -> torch.Tensor:
+        epoch, start, size = self.geom.batch_pos(t)
+        if self._native is not None:
+            if self._b0 is None or not (self._b0 <= t < self._b0 + self.block):
+                import ctypes
+
+                from .. import _native as nat
+
+                nat.check(self._native.dtp_sampler_indices(ctypes.byref(self._cfg), t, self.block,
+                                                           nat.ptr(self._buf), nat.stream_ptr()),
+                          "dtp_sampler_indices")
+                self._b0 = t
+            return self._buf[t - self._b0, :size]
+        if epoch != self._epoch:
+            if self.exact:
+                host = torch.tensor(self._stream.epoch_list(epoch), dtype=torch.int64)
+            else:
+                host = torch.from_numpy(self.geom.epoch_indices(epoch))
+            if self.device.type == "cuda":
+                host = host.pin_memory()
+            self._ep_idx = host.to(self.device, non_blocking=True)
+            self._epoch = epoch
+        return self._ep_idx[start:start + size]

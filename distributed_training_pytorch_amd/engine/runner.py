@@ -25,13 +25,13 @@ import time
 import torch
 import torch.distributed as dist
 
-from ..data.sampler import EpochIndexStream, SamplerGeometry
+from ..data.sampler import BatchIndexer, SamplerGeometry
 from ..data.toy_data import ToyData
 from ..ops.optim import OptimConfig
 from ..parallel import comm_util
 from ..runtime import bootstrap, checkpoint
 from ..runtime.errors import FaultInjector, check_replicas
-from ..utils.logging import MetricLogger, rank_print
+from ..utils.logging import LossRing, MetricLogger, rank_print
 from ..utils.profiling import PhaseTimer
 from ..utils.profiling import enabled as trace_enabled
 
@@ -220,7 +220,9 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     ds = _dataset(config, rank)
     X, Y = ds.device_tensors(device)
     geom = _geom(config, rank, world)
-    idx_stream = EpochIndexStream(geom) if config.sampler == "torch" else None
+    # batch indices on the device: the native sampler kernel, or the exact torch order
+    # uploaded once per epoch (no per-step host index math or copies)
+    indexer = BatchIndexer(geom, device, exact_torch=config.sampler == "torch")
     torch.manual_seed(config.seed)
     out_f = 4 if config.loss == "ce" else 1
     bank = ModelBank(2, hidden=config.hidden, depth=config.depth, out_features=out_f,
@@ -228,6 +230,7 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad,
                   comm=config.comm if config.comm in ("auto", "rccl", "xgmi") else "rccl")
     rank_print(rank, f"engine: module (FlatDDP over {ddp.comm})")
+    from .graph_step import CapturedStep
     opt = FlatOptimizer(bank.flat, bank.flat_grad, _optim(config))
     lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else torch.nn.MSELoss()
     start = 0
@@ -252,13 +255,28 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
         pbar.update(start)
     timer = PhaseTimer(device)
     t0 = time.perf_counter()
-    lbuf = torch.zeros(2, device=device)
-    for it in range(start, config.iters):
-        faults.check(it)
+    # per-step losses stay on the device; the global means are reduced and logged once
+    # per log_every steps (one all-reduce of the chunk, one host sync), with the same
+    # per-step values and keys as the reference's per-step gloo reduce + wandb.log
+    ring = LossRing(max(1, config.log_every), 2, device, world)
+    last = [float("nan")] * 2
+
+    def _flush():
+        nonlocal last
+        for step, (vx, vy) in ring.flush():
+            if rank == 0:
+                logger.log({"loss/lossX": vx}, step=step, commit=False)
+                logger.log({"loss/lossY": vy}, step=step)
+            last = [vx, vy]
+
+    # the batch indices of the current iteration, refreshed before each step (the
+    # captured graph reads this static buffer)
+    idx_static = torch.zeros(geom.batch, dtype=torch.int64, device=device)
+
+    def step_body(size):
+        idx_t = idx_static[:size]
         with timer.phase("data"):
-            idx = idx_stream.indices(it) if idx_stream is not None else geom.indices(it)
-            idx_t = torch.tensor(idx, device=device)
-            x, y = X[idx_t], Y[idx_t]
+            x, y = X.index_select(0, idx_t), Y.index_select(0, idx_t)
             if config.loss == "ce":
                 y = y.view(-1).long()
         bank.zero_grad()
@@ -269,17 +287,28 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
             (lx + ly).backward()  # independent models: one backward, one bucketed all-reduce
         with timer.phase("optimizer"):
             opt.step()
-        with timer.phase("loss_reduce"):
-            lbuf[0], lbuf[1] = lx.detach(), ly.detach()
-            comm_util.all_reduce_(lbuf)
-            lbuf.mul_(1.0 / world)
-        if rank == 0:
-            logger.log({"loss/lossX": lbuf[0].item()}, step=it, commit=False)
-            logger.log({"loss/lossY": lbuf[1].item()}, step=it)
+        ring.put_device(lx, ly)
+
+    # hipGraph replay of the whole iteration (engine/graph_step.py) where it can be
+    # captured: one rank, or RCCL buckets (the xGMI bucket path and gloo are host-driven)
+    graphable = device.type == "cuda" and config.launch != "eager" and not trace_enabled() and (
+        world == 1 or (dist.get_backend() == "nccl" and ddp.comm == "rccl"))
+    stepper = CapturedStep(step_body, device, enabled=graphable, on_abort=ddp.reset_hooks)
+    for it in range(start, config.iters):
+        faults.check(it)
+        size = geom.batch_size_at(it)
+        idx_static[:size].copy_(indexer(it))
+        stepper.run(size)
+        ring.mark(it)
+        if ring.full():
+            with timer.phase("loss_reduce"):
+                _flush()
         if pbar is not None:
             pbar.update(1)
         if config.checkpoint_dir and config.checkpoint_every and (it + 1) % config.checkpoint_every == 0:
+            _flush()
             _save(it + 1)
+    _flush()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     ddp.check_comm()
@@ -290,8 +319,9 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
         check_replicas(bank.flat)
     if config.checkpoint_dir:
         _save(config.iters)
-    return {"final_loss": lbuf.tolist(), "iters": config.iters,
+    return {"final_loss": last, "iters": config.iters,
             "samples_per_s": geom.batch * (config.iters - start) * world / max(dt, 1e-9), "engine": "module",
+            "graph_replays": stepper.replays,
             **({"phases": timer.summary()} if trace_enabled() else {})}
 
 

@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native as nat
+from .gemm import _fused_grad_target, _grad_ready
 
 
 @dataclass(frozen=True)
@@ -138,8 +139,13 @@ def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool
     return out, saved
 
 
-def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: bool = True):
-    """Native backward of one stage. Returns (grad_in or None, grad_params [P])."""
+def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: bool = True,
+                   grad_params: torch.Tensor | None = None):
+    """Native backward of one stage. Returns (grad_in or None, grad_params [P]).
+
+    With ``grad_params`` (a contiguous fp32 [P] span, e.g. the parameters' persistent
+    ``.grad`` views in a flat gradient buffer) the kernel ADDS the parameter gradient
+    into it instead of returning a fresh tensor for autograd to add."""
     lib = nat.require(x.device)
     dev = x.device
     B = x.shape[0]
@@ -150,10 +156,15 @@ def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: b
         _check_f32_cuda("grad_out", grad_out, dev, B * spec.out_features)
     grad_in = torch.empty(B, spec.in_features, device=dev, dtype=torch.float32) if need_grad_in else None
     nblk = (B + 1023) // 1024
-    gp = torch.zeros(spec.P, device=dev, dtype=torch.float32) if nblk > 1 else \
-        torch.empty(spec.P, device=dev, dtype=torch.float32)
+    acc = grad_params is not None
+    if acc:
+        _check_f32_cuda("grad_params", grad_params, dev, spec.P)
+        gp = grad_params
+    else:
+        gp = torch.zeros(spec.P, device=dev, dtype=torch.float32) if nblk > 1 else \
+            torch.empty(spec.P, device=dev, dtype=torch.float32)
     a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), nat.ptr(grad_out),
-                      nat.ptr(grad_in), nat.ptr(gp), None, B, spec.slope)
+                      nat.ptr(grad_in), nat.ptr(gp), None, B, spec.slope, int(acc))
     nat.check(lib.dtp_mlp_stage_bwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_bwd")
     return grad_in, gp
 
@@ -189,6 +200,7 @@ class FusedMLPFunction(torch.autograd.Function):
         out, saved = stage_forward(x, flat, spec, save=True)
         ctx.spec = spec
         ctx.shapes = [p.shape for p in params]
+        ctx.params = params
         ctx.save_for_backward(x, flat, out, saved if saved is not None else torch.empty(0, device=x.device))
         return out
 
@@ -196,8 +208,19 @@ class FusedMLPFunction(torch.autograd.Function):
     def backward(ctx, grad_out):
         x, flat, out, saved = ctx.saved_tensors
         spec = ctx.spec
+        params = ctx.params
+        # parameters whose .grad is a persistent view of one flat gradient span
+        # (ModelBank / FlatDDP, ops.gemm.mark_fused_grad): the kernel adds into it, so
+        # autograd runs no AccumulateGrad add kernel per parameter tensor
+        target = None
+        if all(ctx.needs_input_grad[2:]) and all(_fused_grad_target(p) is not None for p in params):
+            target = _flat_view_of([p.grad for p in params])
         gin, gp = stage_backward(x, flat, spec, out, saved if saved.numel() else None, grad_out,
-                                 need_grad_in=ctx.needs_input_grad[0])
+                                 need_grad_in=ctx.needs_input_grad[0], grad_params=target)
+        if target is not None:
+            for p in params:
+                _grad_ready(p)
+            return (gin, None, *([None] * len(params)))
         grads, o = [], 0
         for shp in ctx.shapes:
             n = 1

@@ -202,6 +202,11 @@ class FlatDDP(nn.Module):
     def zero_grad(self):
         self.flat_grad.zero_()
 
+    def reset_hooks(self):
+        """Forget a backward that never finished (e.g. an aborted graph capture)."""
+        self._works = []
+        self._callback_queued = False
+
     def check_comm(self):
         """Raise if an xGMI all-reduce timed out (one host sync; call at log points)."""
         if self._xgmi is not None:

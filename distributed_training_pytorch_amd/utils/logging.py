@@ -78,3 +78,58 @@ class MetricLogger:
 
 def rank_print(rank: int, *msg) -> None:
     print(f"[Process {rank}]", *msg, flush=True)
+
+
+class LossRing:
+    """Per-step losses kept on the device, reduced across ranks and read back in chunks.
+
+    The reference reduces each loss over gloo and logs it every iteration
+    (``demo.py:114-121``), a host sync per step. Here ``put`` only queues device
+    work (the row is chosen by a device-side slot counter, so ``put_device`` can sit
+    inside a captured hipGraph); ``flush`` runs ONE all-reduce over the whole chunk
+    and ONE device-to-host read, and returns the same per-step global means (sum
+    over ranks / world). Every rank must call ``flush`` at the same steps (it is a
+    collective).
+    """
+
+    def __init__(self, cap: int, width: int, device, world: int = 1, group=None):
+        import torch
+
+        self.buf = torch.zeros(cap, width, dtype=torch.float32, device=device)
+        self.slot = torch.zeros(1, dtype=torch.int64, device=device)
+        self.world = world
+        self.group = group
+        self.steps: list[int] = []
+
+    def put_device(self, *values) -> None:
+        """Device half of ``put`` (graph-capturable): row[slot] = values; slot += 1."""
+        import torch
+
+        row = torch.stack([v.detach().reshape(()).float() for v in values]).view(1, -1)
+        self.buf.index_copy_(0, self.slot, row)
+        self.slot.add_(1)
+
+    def mark(self, step: int) -> None:
+        """Host half of ``put``: the row just written holds ``step``."""
+        self.steps.append(step)
+
+    def put(self, step: int, *values) -> None:
+        self.put_device(*values)
+        self.mark(step)
+
+    def full(self) -> bool:
+        return len(self.steps) == self.buf.shape[0]
+
+    def flush(self) -> list[tuple[int, list[float]]]:
+        if not self.steps:
+            return []
+        from ..parallel import comm_util
+
+        k = len(self.steps)
+        chunk = self.buf[:k]
+        comm_util.all_reduce_(chunk, self.group)
+        vals = (chunk / self.world).cpu().tolist()
+        out = list(zip(self.steps, vals))
+        self.steps = []
+        self.slot.zero_()
+        return out

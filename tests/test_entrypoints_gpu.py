@@ -66,6 +66,18 @@ def test_demo_module_engine_on_gpu(tmp_path):
     assert all(0.0 < l < 4.0 for l in s["final_loss"]), s
 
 
+def test_module_engine_graph_replay_equals_eager(tmp_path):
+    """The module engine's hipGraph-captured iteration (engine/graph_step.py) computes
+    exactly what the eager iteration does; batch 200 of 512 samples gives a partial
+    last batch, i.e. a second captured graph."""
+    args = ["demo.py", "--engine", "module", "--iters", "60", "--batch_size", "200", "--seed", "3", "--dry_run",
+            "--no_progress", "--log_every", "7", "--log_dir", str(tmp_path)]
+    g = _summary(_run(args))
+    e = _summary(_run(args + ["--launch", "eager"]))
+    assert g["graph_replays"] >= 50 and e["graph_replays"] == 0, (g, e)
+    assert g["final_loss"] == e["final_loss"], (g, e)
+
+
 def test_demo_mpiexec_env_on_gpu(tmp_path):
     env = {"OMPI_COMM_WORLD_RANK": "0", "OMPI_COMM_WORLD_SIZE": "1", "OMPI_COMM_WORLD_LOCAL_RANK": "0",
            "OMPI_COMM_WORLD_LOCAL_SIZE": "1", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_port())}
