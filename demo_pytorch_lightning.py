@@ -60,6 +60,8 @@ def get_args(argv=None):
     p.add_argument("--root_dir", type=str, default=None)
     p.add_argument("--no_progress", action="store_true")
     p.add_argument("--use_lightning", action="store_true", help="use pytorch_lightning if it is installed")
+    p.add_argument("--no_graphs", action="store_true",
+                   help="in-repo Trainer: run every batch eagerly instead of replaying it as a hipGraph")
     return p.parse_args(argv)
 
 
@@ -79,16 +81,18 @@ def main(argv=None):
             TrainerCls = pl.Trainer
         except ImportError:
             print("pytorch_lightning not installed; using the in-repo Trainer", flush=True)
+    extra = {"seed": a.seed, "use_graphs": not a.no_graphs} if TrainerCls is Trainer else {}
     trainer = TrainerCls(gpus=a.gpus, num_nodes=a.nnodes, max_steps=a.steps, precision=32, accelerator=accel,
                          log_every_n_steps=min(50, len(dl) / a.batch_size), strategy="ddp",
-                         default_root_dir=a.root_dir, enable_progress_bar=not a.no_progress, seed=a.seed)
+                         default_root_dir=a.root_dir, enable_progress_bar=not a.no_progress, **extra)
     trainer.fit(model, dl)
     if getattr(trainer, "global_rank", 0) == 0:
         sps = None
         if getattr(trainer, "fit_time", None):
             sps = trainer.global_step * a.batch_size * getattr(trainer, "world_size", 1) / trainer.fit_time
         print(f"[Process 0] summary: {{'global_step': {trainer.global_step}, 'metrics': {trainer.callback_metrics}, "
-              f"'checkpoint': {trainer.checkpoint_path!r}, 'samples_per_s': {sps}}}", flush=True)
+              f"'checkpoint': {trainer.checkpoint_path!r}, 'samples_per_s': {sps}, "
+              f"'graph_replays': {getattr(trainer, 'graph_replays', 0)}}}", flush=True)
     if hasattr(trainer, "teardown"):
         trainer.teardown()
 

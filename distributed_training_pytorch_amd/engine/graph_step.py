@@ -82,6 +82,10 @@ class CapturedStep:
         graph.replay()
         self.replays += 1
 
+    def is_captured(self, key: Hashable) -> bool:
+        g = self._graphs.get(key)
+        return g is not None and g is not False
+
     @property
     def captured(self) -> int:
         return sum(1 for g in self._graphs.values() if g is not None and g is not False)

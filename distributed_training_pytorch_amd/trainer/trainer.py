@@ -95,7 +95,7 @@ class Trainer:
                  precision: int = 32, accelerator: str | None = None, strategy: str | None = None,
                  log_every_n_steps: float = 50, default_root_dir: str | None = None,
                  enable_checkpointing: bool = True, enable_progress_bar: bool = True, seed: int | None = None,
-                 **unused):
+                 use_graphs: bool = True, **unused):
         if precision not in (32, "32"):
             raise NotImplementedError("the toy MLP path trains in fp32 (precision=32), like the reference")
         self.gpus = gpus
@@ -109,6 +109,8 @@ class Trainer:
         self.enable_checkpointing = enable_checkpointing
         self.enable_progress_bar = enable_progress_bar
         self.seed = seed
+        self.use_graphs = use_graphs  # replay each batch's optimizer steps as a hipGraph (GPU)
+        self.graph_replays = 0
         self.global_step = 0
         self.current_epoch = 0
         self.callback_metrics: dict = {}
@@ -155,11 +157,15 @@ class Trainer:
             torch.manual_seed(self.seed)
         model.trainer = self
         model.to(self.device)
-        ddp = FlatDDP(model) if self.world_size > 1 else None
+        # the flat gradient buffer of FlatDDP also serves one process: fused kernels add
+        # their parameter gradients into its views in place (no AccumulateGrad adds)
+        ddp = FlatDDP(model) if (self.world_size > 1 or self.device.type == "cuda") else None
         opts = model.configure_optimizers()
         if not isinstance(opts, (list, tuple)):
             opts = [opts]
         loader = self._loader(dl)
+        stepper, static = self._batch_stepper(model, ddp, opts)
+        logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
         pbar = None
         if self.enable_progress_bar and self.global_rank == 0:
@@ -179,21 +185,22 @@ class Trainer:
                 loader.sampler.set_epoch(self.current_epoch)
             for batch_idx, batch in enumerate(loader):
                 batch = [b.to(self.device, non_blocking=True) for b in batch]
-                for oi, opt in enumerate(opts):
-                    if len(opts) > 1:
-                        model.toggle_optimizer(opt, oi, opts)
-                    if ddp is not None:
-                        ddp.zero_grad()
+                if stepper is not None and self._static_ok(static, batch):
+                    key = tuple(tuple(b.shape) for b in batch)
+                    if key not in static:
+                        static[key] = [b.clone() for b in batch]
+                    for dst, src in zip(static[key], batch):
+                        dst.copy_(src)
+                    self._cur_batch_idx = batch_idx  # read by the body only while capturing
+                    replay = stepper.is_captured(key)
+                    stepper.run(key)
+                    # logged tensors of a replay are that key's graph outputs (refreshed in place)
+                    if replay:
+                        model._logged.update(logged_by_key[key])
                     else:
-                        opt.zero_grad(set_to_none=False)
-                    out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
-                        model.training_step(batch, batch_idx)
-                    loss = out["loss"] if isinstance(out, dict) else out
-                    loss.backward()
-                    opt.step()
-                    if len(opts) > 1:
-                        model.untoggle_optimizer(oi)
-                    model._logged[f"train_loss_opt{oi}"] = loss.detach()
+                        logged_by_key[key] = dict(model._logged)
+                else:
+                    self._optimizer_steps(model, ddp, opts, batch, batch_idx)
                 self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
                 if self.global_step % self.log_every_n_steps == 0:
                     metrics = {k: v for k, v in model._logged.items()}
@@ -213,6 +220,8 @@ class Trainer:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         self.fit_time = time.perf_counter() - t0
+        if stepper is not None:
+            self.graph_replays = stepper.replays
         if pbar is not None:
             pbar.close()
         model.on_train_end()
@@ -228,6 +237,61 @@ class Trainer:
             self.checkpoint_path = str(path)
         logger.close()
         return self
+
+    def _optimizer_steps(self, model, ddp, opts, batch, batch_idx):
+        """One batch: for each optimizer (PL 1.5): toggle, zero_grad, training_step,
+        backward, step, untoggle."""
+        for oi, opt in enumerate(opts):
+            if len(opts) > 1:
+                model.toggle_optimizer(opt, oi, opts)
+            if ddp is not None:
+                ddp.zero_grad()
+            else:
+                opt.zero_grad(set_to_none=False)
+            out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
+                model.training_step(batch, batch_idx)
+            loss = out["loss"] if isinstance(out, dict) else out
+            loss.backward()
+            opt.step()
+            if len(opts) > 1:
+                model.untoggle_optimizer(oi)
+            model._logged[f"train_loss_opt{oi}"] = loss.detach()
+
+    @staticmethod
+    def _static_ok(static, batch) -> bool:
+        return all(isinstance(b, torch.Tensor) and b.is_cuda for b in batch)
+
+    def _batch_stepper(self, model, ddp, opts):
+        """A CapturedStep replaying one batch's optimizer steps as a hipGraph, when the
+        run allows it: a GPU, one rank or RCCL buckets, and optimizers that can keep
+        their step counts on the device (torch's ``capturable`` param-group flag)."""
+        if not (self.use_graphs and self.device.type == "cuda"):
+            return None, None
+        if ddp is not None and self.world_size > 1 and not (dist.get_backend() == "nccl" and ddp.comm == "rccl"):
+            return None, None
+        for opt in opts:
+            if not all("capturable" in g for g in opt.param_groups) and not isinstance(opt, torch.optim.SGD):
+                return None, None
+        for opt in opts:
+            for g in opt.param_groups:
+                if "capturable" in g:
+                    g["capturable"] = True
+        from ..engine.graph_step import CapturedStep
+
+        static: dict = {}
+
+        def body(key):
+            self._optimizer_steps(model, ddp, opts, static[key], self._cur_batch_idx)
+
+        def abort():
+            if getattr(model, "_toggled", None):
+                model.untoggle_optimizer(-1)
+            if ddp is not None:
+                ddp.reset_hooks()
+
+        stepper = CapturedStep(body, self.device, on_abort=abort)
+        self._stepper = stepper
+        return stepper, static
 
     def teardown(self):
         if dist.is_initialized():

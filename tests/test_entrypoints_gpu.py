@@ -104,3 +104,14 @@ def test_demo_lightning_trainer_on_gpu(tmp_path):
     assert ckpts, out[-2000:]
     metrics = list(tmp_path.glob("lightning_logs/version_*/metrics.csv"))
     assert metrics and metrics[0].read_text().count("\n") > 1
+
+
+def test_lightning_trainer_graph_replay_matches_eager(tmp_path):
+    """The Trainer's hipGraph batch replay (two optimizers, toggled params, capturable
+    Adam) logs the same losses as its eager batches."""
+    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "64", "--seed", "0", "--no_progress"]
+    g = _summary(_run(base + ["--root_dir", str(tmp_path / "g")], finished=False))
+    e = _summary(_run(base + ["--root_dir", str(tmp_path / "e"), "--no_graphs"], finished=False))
+    assert g["graph_replays"] >= 50 and e["graph_replays"] == 0, (g, e)
+    for k, v in e["metrics"].items():
+        assert abs(g["metrics"][k] - v) <= 1e-4 * max(1.0, abs(v)), (k, g["metrics"], e["metrics"])
