@@ -450,6 +450,28 @@ class FusedTrainer:
         ids = torch.arange(t0, t1) % cap
         return self.loss_log.index_select(0, ids.to(self.loss_log.device)).cpu()
 
+    def losses_async(self, t0: int, t1: int) -> "LossReadback":
+        """Queue a copy of the losses of steps [t0, t1) (and the xGMI status word) to
+        pinned host memory behind the work already on the stream; ``.wait()`` returns
+        them as a list of [n_models] rows without syncing on anything queued later."""
+        cap = self.loss_log.shape[0]
+        if t1 - t0 > cap:
+            t0 = t1 - cap
+        a, b = t0 % cap, t1 - t0
+        if self.device.type != "cuda":
+            rows = torch.cat([self.loss_log[a:], self.loss_log[:max(0, a + b - cap)]])[:b].clone()
+            return LossReadback(rows, None, None, self.rank)
+        src = self.loss_log[a:a + b] if a + b <= cap else torch.cat([self.loss_log[a:], self.loss_log[:a + b - cap]])
+        host = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+        host.copy_(src, non_blocking=True)
+        st = None
+        if self._xgmi is not None:
+            st = torch.empty(2, dtype=torch.int32, pin_memory=True)
+            st.copy_(self._xgmi.status[:2], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return LossReadback(host, st, ev, self.rank)
+
     def state_dict(self) -> dict:
         return {"params": self.params.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(),
                 "step": self.step_ctr.cpu(), "t": self.t, "spec": self.spec.__dict__,
@@ -479,3 +501,18 @@ class FusedTrainer:
                 comm_util.barrier(self.group)
             self._xgmi.close()
             self._xgmi = None
+
+
+class LossReadback:
+    """Handle of :meth:`FusedTrainer.losses_async`."""
+
+    def __init__(self, rows: torch.Tensor, status: torch.Tensor | None, event, rank: int):
+        self.rows, self.status, self.event, self.rank = rows, status, event, rank
+
+    def wait(self) -> list[list[float]]:
+        if self.event is not None:
+            self.event.synchronize()
+        if self.status is not None and int(self.status[0]):
+            raise RuntimeError(f"xGMI exchange timed out on rank {self.rank} at epoch {int(self.status[1])} "
+                               "(peer not responding)")
+        return self.rows.tolist()

@@ -170,6 +170,25 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
     it = start
     chunk = max(1, min(config.log_every, config.steps_per_launch))
     timer = PhaseTimer(device)
+
+    def ckpt_due(i):
+        return bool(config.checkpoint_dir and config.checkpoint_every and i % config.checkpoint_every == 0)
+
+    # Chunks are pipelined: chunk k+1 is queued on the GPU before the host logs chunk
+    # k, whose losses (and the xGMI status word) were copied to pinned memory behind
+    # it, so logging overlaps the next chunk instead of idling the GPU.
+    pending = None
+
+    def process(p):
+        it0, n, handle = p
+        with timer.phase("loss_readback"):
+            ls = handle.wait()  # raises on a sticky xGMI timeout: never train on partial sums
+        for k in range(n):
+            logger.log({"loss/lossX": ls[k][0]}, step=it0 + k, commit=False)
+            logger.log({"loss/lossY": ls[k][1]}, step=it0 + k)
+        if pbar is not None:
+            pbar.update(n)
+
     t0 = time.perf_counter()
     while it < config.iters:
         n = min(chunk, config.iters - it)
@@ -178,17 +197,17 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
         if n > 0:
             with timer.phase("train_chunk"):
                 tr.train(n)
-            with timer.phase("loss_readback"):
-                ls = tr.losses(it, it + n)  # one host sync per chunk
-                tr.check_comm()  # sticky xGMI timeout word: raise now, never train on partial sums
-            for k in range(n):
-                logger.log({"loss/lossX": ls[k, 0].item()}, step=it + k, commit=False)
-                logger.log({"loss/lossY": ls[k, 1].item()}, step=it + k)
+            handle = tr.losses_async(it, it + n)
+            if pending is not None:
+                process(pending)
+            pending = (it, n, handle)
             it += n
-            if pbar is not None:
-                pbar.update(n)
+        if pending is not None and (it >= config.iters or ckpt_due(it) or
+                                    (faults.armed() and it >= config.fail_at_iter)):
+            process(pending)
+            pending = None
         faults.check(it)
-        if config.checkpoint_dir and config.checkpoint_every and it % config.checkpoint_every == 0:
+        if ckpt_due(it):
             tr.synchronize()
             checkpoint.save({**tr.state_dict(), "engine": "fused", "config": vars(config)},
                             config.checkpoint_dir, it)
@@ -196,6 +215,8 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
             # timeout), not inside the next launch's first in-kernel xGMI exchange,
             # whose bounded spin a slow checkpoint filesystem could outlast
             comm_util.barrier()
+    if pending is not None:
+        process(pending)
     tr.synchronize()
     dt = time.perf_counter() - t0
     if pbar is not None:
