@@ -274,8 +274,14 @@ def check(rc: int, what: str):
 
 
 def stream_ptr(stream: torch.cuda.Stream | None = None) -> int:
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return int(s.cuda_stream)
+    """Raw hipStream_t of ``stream`` or of the current device's current stream (the
+    capture stream inside ``torch.cuda.graph``).  The default path reads it straight
+    from c10: ``torch.cuda.current_stream()`` with no device resolves the device through
+    ``torch.cuda.is_available()``, a ``hipGetDeviceCount`` per call (~30 us on the
+    MI355X box), which was the largest host cost of every native op launch."""
+    if stream is not None:
+        return int(stream.cuda_stream)
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def raw_stream(device_index: int) -> int:

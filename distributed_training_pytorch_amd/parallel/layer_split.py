@@ -76,6 +76,7 @@ class _PeerStageFn(torch.autograd.Function):
                 ev.record(torch.cuda.current_stream(src))
                 torch.cuda.current_stream(dst).wait_event(ev)
         ctx.spec, ctx.src, ctx.dst = spec, src, dst
+        ctx.param = flat  # the stage's Parameter: its persistent .grad takes the kernel's in-place add
         ctx.save_for_backward(x, flat, out, saved if saved is not None else torch.empty(0, device=src))
         return out_dst
 
@@ -87,14 +88,19 @@ class _PeerStageFn(torch.autograd.Function):
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dst))
             torch.cuda.current_stream(src).wait_event(ev)
+        g = getattr(ctx.param, "grad", None)
+        inplace = (ctx.needs_input_grad[1] and g is not None and g.dtype == torch.float32 and g.is_contiguous()
+                   and g.device == src)
         with torch.cuda.device(src):
             gin, gp = stage_backward(x, flat, ctx.spec, out, saved if saved.numel() else None,
-                                     grad_out.contiguous(), need_grad_in=ctx.needs_input_grad[0])
+                                     grad_out.contiguous(), need_grad_in=ctx.needs_input_grad[0],
+                                     grad_params=g if inplace else None)
             if dst != src:
                 ev2 = torch.cuda.Event()
                 ev2.record(torch.cuda.current_stream(src))
                 torch.cuda.current_stream(dst).wait_event(ev2)
-        return gin, gp, None, None
+        # in place: the kernel already added into .grad, autograd has nothing to accumulate
+        return gin, (None if inplace else gp), None, None
 
 
 class LayerSplitMLP(nn.Module):
