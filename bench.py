@@ -114,22 +114,24 @@ def main():
 
         dbar = DeviceBarrier(dev)
 
-    def barrier():
+    def sync_barrier():
+        """synchronize + all-rank barrier.  The device barrier is queued on the stream
+        right behind the work before it, so one synchronize covers both (no extra
+        launch-and-wait round trip); a process-group barrier follows the synchronize."""
         if dbar is not None:
             dbar()
             sync()
         else:
+            sync()
             dist_env.barrier()
 
     # warmup (untimed)
     train(a.warmup)
-    sync()
-    barrier()
+    sync_barrier()
     sync()
     t0 = time.perf_counter()
     train(a.steps)
-    sync()
-    barrier()
+    sync_barrier()
     t1 = time.perf_counter()
     elapsed = dist_env.allreduce_max(t1 - t0, dev)
     ms_per_step = 1e3 * elapsed / a.steps

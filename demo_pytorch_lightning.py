@@ -62,6 +62,8 @@ def get_args(argv=None):
     p.add_argument("--use_lightning", action="store_true", help="use pytorch_lightning if it is installed")
     p.add_argument("--no_graphs", action="store_true",
                    help="in-repo Trainer: run every batch eagerly instead of replaying it as a hipGraph")
+    p.add_argument("--torch_optimizers", action="store_true",
+                   help="in-repo Trainer: step the torch optimizers themselves, not the flat-optimizer kernel")
     return p.parse_args(argv)
 
 
@@ -81,7 +83,8 @@ def main(argv=None):
             TrainerCls = pl.Trainer
         except ImportError:
             print("pytorch_lightning not installed; using the in-repo Trainer", flush=True)
-    extra = {"seed": a.seed, "use_graphs": not a.no_graphs} if TrainerCls is Trainer else {}
+    extra = {"seed": a.seed, "use_graphs": not a.no_graphs, "native_optimizers": not a.torch_optimizers} \
+        if TrainerCls is Trainer else {}
     trainer = TrainerCls(gpus=a.gpus, num_nodes=a.nnodes, max_steps=a.steps, precision=32, accelerator=accel,
                          log_every_n_steps=min(50, len(dl) / a.batch_size), strategy="ddp",
                          default_root_dir=a.root_dir, enable_progress_bar=not a.no_progress, **extra)

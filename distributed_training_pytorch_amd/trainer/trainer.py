@@ -95,7 +95,7 @@ class Trainer:
                  precision: int = 32, accelerator: str | None = None, strategy: str | None = None,
                  log_every_n_steps: float = 50, default_root_dir: str | None = None,
                  enable_checkpointing: bool = True, enable_progress_bar: bool = True, seed: int | None = None,
-                 use_graphs: bool = True, **unused):
+                 use_graphs: bool = True, native_optimizers: bool = True, **unused):
         if precision not in (32, "32"):
             raise NotImplementedError("the toy MLP path trains in fp32 (precision=32), like the reference")
         self.gpus = gpus
@@ -110,6 +110,9 @@ class Trainer:
         self.enable_progress_bar = enable_progress_bar
         self.seed = seed
         self.use_graphs = use_graphs  # replay each batch's optimizer steps as a hipGraph (GPU)
+        # run a plain torch Adam/SGD over a flat-buffer span as ONE flat-optimizer kernel (GPU)
+        self.native_optimizers = native_optimizers
+        self._flat_opts: list = []
         self.graph_replays = 0
         self.global_step = 0
         self.current_epoch = 0
@@ -164,6 +167,7 @@ class Trainer:
         if not isinstance(opts, (list, tuple)):
             opts = [opts]
         loader = self._loader(dl)
+        self._flat_opts = [_flat_optimizer_for(o, ddp) if self.native_optimizers else None for o in opts]
         stepper, static = self._batch_stepper(model, ddp, opts)
         logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
@@ -225,6 +229,9 @@ class Trainer:
         if pbar is not None:
             pbar.close()
         model.on_train_end()
+        for fo in self._flat_opts:
+            if fo is not None:
+                fo.export_state()  # the user's torch optimizers hold the trained state again
         if self.enable_checkpointing and logger.dir is not None:
             ck = logger.dir / "checkpoints"
             ck.mkdir(exist_ok=True)
@@ -252,7 +259,11 @@ class Trainer:
                 model.training_step(batch, batch_idx)
             loss = out["loss"] if isinstance(out, dict) else out
             loss.backward()
-            opt.step()
+            flat = self._flat_opts[oi] if oi < len(self._flat_opts) else None
+            if flat is not None:
+                flat.step()
+            else:
+                opt.step()
             if len(opts) > 1:
                 model.untoggle_optimizer(oi)
             model._logged[f"train_loss_opt{oi}"] = loss.detach()
@@ -297,3 +308,75 @@ class Trainer:
         if dist.is_initialized():
             comm_util.barrier()
             dist.destroy_process_group()
+
+
+class _FlatTorchOptimizer:
+    """A user's plain ``torch.optim.Adam`` / ``SGD`` run as ONE flat-optimizer kernel
+    (``csrc/optim.hip``, the element-for-element mirror of torch's math) over the span
+    of the flat parameter buffer its single param group covers, instead of torch's
+    ~5 multi-tensor launches plus per-parameter step bookkeeping.  The moments live
+    in flat buffers; ``export_state`` writes them back into ``opt.state`` in torch's
+    own format (checkpoints, continued use of the optimizer)."""
+
+    def __init__(self, opt, params, flat_p, flat_g, cfg):
+        from ..ops.optim import FlatOptimizer
+
+        self.opt = opt
+        self.params = params
+        self.cfg = cfg
+        self.flat = FlatOptimizer(flat_p, flat_g, cfg)
+
+    def step(self):
+        self.flat.step()
+
+    def export_state(self):
+        step = int(self.flat.step_ctr[0].item())
+        if step == 0:
+            return
+        group = self.opt.param_groups[0]
+        o = 0
+        m, v = self.flat.m.view(-1), self.flat.v.view(-1)
+        for p in self.params:
+            n = p.numel()
+            st = self.opt.state[p]
+            if self.cfg.name == "adam":
+                cap = bool(group.get("capturable", False))
+                st["step"] = torch.tensor(float(step), dtype=torch.float32, device=p.device if cap else "cpu")
+                st["exp_avg"] = m[o:o + n].view_as(p).clone()
+                st["exp_avg_sq"] = v[o:o + n].view_as(p).clone()
+            elif self.cfg.momentum:
+                st["momentum_buffer"] = m[o:o + n].view_as(p).clone()
+            o += n
+
+
+def _flat_optimizer_for(opt, ddp):
+    """_FlatTorchOptimizer for ``opt`` if it is a plain Adam/SGD whose one param group
+    is a contiguous span of the flat buffers on a GPU, else None (torch's step runs)."""
+    from ..ops.mlp import _flat_view_of
+    from ..ops.optim import OptimConfig
+
+    if ddp is None or not ddp.flat_params.is_cuda or len(opt.param_groups) != 1 or opt.state:
+        return None
+    g = opt.param_groups[0]
+    lr = g.get("lr")
+    if isinstance(lr, torch.Tensor) or g.get("maximize") or g.get("differentiable"):
+        return None
+    if type(opt) is torch.optim.Adam:
+        if g.get("amsgrad") or g.get("decoupled_weight_decay"):
+            return None
+        cfg = OptimConfig("adam", float(lr), tuple(float(b) for b in g["betas"]), float(g["eps"]),
+                          float(g["weight_decay"]))
+    elif type(opt) is torch.optim.SGD:
+        if g.get("nesterov") or g.get("dampening", 0):
+            return None
+        cfg = OptimConfig("sgd", float(lr), weight_decay=float(g["weight_decay"]), momentum=float(g["momentum"]))
+    else:
+        return None
+    params = list(g["params"])
+    if not params or any(p.dtype != torch.float32 or p.grad is None for p in params):
+        return None
+    flat_p = _flat_view_of([p.data for p in params])
+    flat_g = _flat_view_of([p.grad for p in params])
+    if flat_p is None or flat_g is None:
+        return None
+    return _FlatTorchOptimizer(opt, params, flat_p, flat_g, cfg)
