@@ -71,7 +71,11 @@ def main():
     if torch.cuda.device_count() > 0:  # counting devices does not initialise the GPU
         from distributed_training_pytorch_amd import _native
 
-        _native.set_wait_mode()  # DTP_WAIT_MODE; before the first GPU touch
+        # host threads spin on GPU completion (DTP_WAIT_MODE overrides; before the first
+        # GPU touch): the timed region ends in a synchronize, and a spinning waiter
+        # returns sooner than an interrupt-woken one (K=20 A/B, 8 interleaved runs
+        # each: median 5.55 vs 5.65 us/step, profiles/r2_s3/ab_wait.txt)
+        _native.set_wait_mode(os.environ.get("DTP_WAIT_MODE", "spin"))
     if a.share_gpu and torch.cuda.device_count() > 0:
         os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
     rank, world, local_rank = dist_env.init_from_env(backend="gloo" if a.share_gpu else None,
