@@ -162,7 +162,9 @@ class Trainer:
         model.to(self.device)
         # the flat gradient buffer of FlatDDP also serves one process: fused kernels add
         # their parameter gradients into its views in place (no AccumulateGrad adds)
-        ddp = FlatDDP(model) if (self.world_size > 1 or self.device.type == "cuda") else None
+        single_ok = self.device.type == "cuda" and all(
+            p.dtype == torch.float32 and p.device == self.device for p in model.parameters() if p.requires_grad)
+        ddp = FlatDDP(model) if (self.world_size > 1 or single_ok) else None
         opts = model.configure_optimizers()
         if not isinstance(opts, (list, tuple)):
             opts = [opts]
@@ -275,7 +277,13 @@ class Trainer:
     def _batch_stepper(self, model, ddp, opts):
         """A CapturedStep replaying one batch's optimizer steps as a hipGraph, when the
         run allows it: a GPU, one rank or RCCL buckets, and optimizers that can keep
-        their step counts on the device (torch's ``capturable`` param-group flag)."""
+        their step counts on the device (torch's ``capturable`` param-group flag).
+
+        What a replay repeats is what the capture recorded: device work on the static
+        batch buffers.  Host-side decisions inside ``training_step`` (e.g. on
+        ``batch_idx`` or a Python counter) are frozen at capture time, and a step that
+        syncs with the host cannot be captured (that batch shape then runs eagerly);
+        ``Trainer(use_graphs=False)`` runs every batch eagerly."""
         if not (self.use_graphs and self.device.type == "cuda"):
             return None, None
         if ddp is not None and self.world_size > 1 and not (dist.get_backend() == "nccl" and ddp.comm == "rccl"):
