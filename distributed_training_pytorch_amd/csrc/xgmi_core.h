@@ -42,6 +42,13 @@ DTP_DEV unsigned long long load_granule_sys(const unsigned long long* p) {
 // largest world the in-kernel exchange serves (one node: 8 GPUs, 7 xGMI links each)
 constexpr int kXgmiMaxWorld = 8;
 
+#ifndef DTP_XGMI_PIPE_POLL
+// 1: software-pipelined polls (next poll in flight while the previous one is checked).
+// Measured slower in the one-GPU rehearsal (2 ranks 7.6 vs 6.6 us/step, 8 ranks 12.4 vs
+// 10.0; profiles/r2_s3/ab_poll.txt), so the default is the plain poll-wait-check-sleep loop.
+#define DTP_XGMI_PIPE_POLL 0
+#endif
+
 // ---- fused-step exchange: 16-byte granules -----------------------------------
 // The fused train step owns its parameters in blocks: thread t holds parameters
 // NPT*t .. NPT*t + NPT-1 (P = total).  Each thread publishes its NPT gradient values
@@ -127,18 +134,24 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
       if (r < W && r != R && mine_k(k)) pending |= 1ull << (r * (GPT + 1) + k);
     }
   }
-  while (pending && !dead) {
-    u32x4 x[kXgmiMaxWorld][GPT + 1];
+  // one poll: the pending granules requested at once (absent ones read as zero)
+  auto issue = [&](u32x4 (&x)[kXgmiMaxWorld][GPT + 1], uint64_t pend) {
+    // compiler-only memory clobber (no instruction, no wait): a poll is never merged
+    // with, or hoisted above, an earlier poll of the same granules
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int r = 0; r < kXgmiMaxWorld; ++r) {
 #pragma unroll
       for (int k = 0; k <= GPT; ++k) {
         x[r][k] = u32x4{0u, 0u, 0u, 0u};
-        if ((pending >> (r * (GPT + 1) + k)) & 1ull)
+        if ((pend >> (r * (GPT + 1) + k)) & 1ull)
           x[r][k] = __builtin_amdgcn_raw_buffer_load_b128(ms, (int)(((base + r) * slot + gidx(k)) * 16), 0,
                                                           kSysCoherent);
       }
     }
+  };
+  // accept every still-pending granule of a poll whose tag and check word match
+  auto consume = [&](const u32x4 (&x)[kXgmiMaxWorld][GPT + 1]) {
 #pragma unroll
     for (int r = 0; r < kXgmiMaxWorld; ++r) {
 #pragma unroll
@@ -151,17 +164,53 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
         }
       }
     }
-    if (!pending) break;
-    if (__builtin_amdgcn_s_memrealtime() > deadline) {
-      dead = true;
-      if (a.status) {
-        atomicExch(&a.status[0], 1);
-        atomicExch(&a.status[1], (int)epoch);
+  };
+  auto expired = [&]() {
+    if (__builtin_amdgcn_s_memrealtime() <= deadline) return false;
+    if (a.status) {
+      atomicExch(&a.status[0], 1);
+      atomicExch(&a.status[1], (int)epoch);
+    }
+    return true;
+  };
+#if DTP_XGMI_PIPE_POLL
+  // Software-pipelined polling: the next poll is in flight while the previous one is
+  // checked (the compiler's vmcnt waits only for the older loads), so a granule is
+  // seen about one memory round trip after it lands instead of up to two.  A poll
+  // issued for a granule that an older poll already accepted is simply ignored.
+  if (pending && !dead) {
+    u32x4 xa[kXgmiMaxWorld][GPT + 1], xb[kXgmiMaxWorld][GPT + 1];
+    issue(xa, pending);
+    while (true) {
+      issue(xb, pending);
+      consume(xa);
+      if (!pending) break;
+      if (expired()) {
+        dead = true;
+        break;
       }
+      issue(xa, pending);
+      consume(xb);
+      if (!pending) break;
+      if (expired()) {
+        dead = true;
+        break;
+      }
+    }
+  }
+#else
+  while (pending && !dead) {
+    u32x4 x[kXgmiMaxWorld][GPT + 1];
+    issue(x, pending);
+    consume(x);
+    if (!pending) break;
+    if (expired()) {
+      dead = true;
       break;
     }
     __builtin_amdgcn_s_sleep(1);
   }
+#endif
   // sum in rank order 0..W-1 (bitwise identical on every rank; absent ranks add +0)
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
