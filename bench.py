@@ -8,9 +8,12 @@ shuffle, global mean loss reduced every step.  One "step" = one iteration of
 ``demo.py:99-128`` on every rank: sample the batch, forward+backward both
 models, all-reduce gradients, Adam update of both models, reduce the loss.
 
-Scaling: ``weak`` (default) keeps 512 synthetic samples per rank
-(n = 512*W, per-rank batch 256, global batch 256*W);  ``strong`` reproduces
-the reference's fixed 512-sample set (per-rank batch 512/W capped at 256).
+Scaling: ``strong`` (default) is the reference workload at every N: ONE fixed
+512-sample set split by the DistributedSampler, per-rank batch ceil(512/W)
+capped at 256 -> 256 / 256 / 128 / 64 at W = 1 / 2 / 4 / 8, global batch 256
+(W=1) or 512 (``demo.py:141-148``; BASELINE.md workload table).  ``weak`` keeps
+512 samples per rank instead (n = 512*W, per-rank batch 256) -- a config the
+reference never ran, kept as an extra.
 
 Usage: python bench.py --gpus N --steps K --warmup W   (N>1 under torchrun)
 Prints ONE JSON line on rank 0.
@@ -35,7 +38,8 @@ from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, 
 from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC  # noqa: E402
 from distributed_training_pytorch_amd.ops.optim import OptimConfig  # noqa: E402
-from distributed_training_pytorch_amd.utils import dist_env  # noqa: E402
+from distributed_training_pytorch_amd.parallel import comm_util  # noqa: E402
+from distributed_training_pytorch_amd.runtime import bootstrap  # noqa: E402
 
 METRIC = "samples/sec (whole node) toy MLP DDP at 1/2/4/8 MI355X; scaling efficiency"
 # The reference publishes no numbers, so the baseline is its loop
@@ -56,7 +60,7 @@ def parse():
     ap.add_argument("--launch", choices=["persistent", "graph", "eager"], default="persistent")
     ap.add_argument("--steps-per-launch", type=int, default=1000)
     ap.add_argument("--comm", choices=["auto", "rccl", "xgmi"], default="auto")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
@@ -76,15 +80,19 @@ def main():
         # returns sooner than an interrupt-woken one (K=20 A/B, 8 interleaved runs
         # each: median 5.55 vs 5.65 us/step, profiles/r2_s3/ab_wait.txt)
         _native.set_wait_mode(os.environ.get("DTP_WAIT_MODE", "spin"))
-    if a.share_gpu and torch.cuda.device_count() > 0:
-        os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
-    rank, world, local_rank = dist_env.init_from_env(backend="gloo" if a.share_gpu else None,
-                                                     single_rank_pg=a.impl == "stock")
+    # the demos' launch path (runtime/bootstrap.py): torchrun / SLURM / MPI env
+    # discovery, device binding, process-group init
+    bootstrap.configure_collective_env()
+    env = bootstrap.detect()
+    ndev = torch.cuda.device_count()
+    if a.share_gpu and ndev > 0:
+        env.local_rank %= ndev
+    rank, world = env.rank, env.world_size
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
-    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
-    if dev.type == "cuda":
-        torch.cuda.set_device(dev)
+    dev = bootstrap.bind_device(env)
+    if world > 1 or a.impl == "stock":  # the stock loop wraps its models in torch DDP even at W=1
+        bootstrap.init_process_group(env, "gloo" if (a.share_gpu or dev.type == "cpu") else "nccl", dev)
     n = 512 * world if a.scaling == "weak" else 512
     ds = ToyData(n=n, seed=a.seed)
 
@@ -127,7 +135,7 @@ def main():
             sync()
         else:
             sync()
-            dist_env.barrier()
+            comm_util.barrier()
 
     # warmup (untimed)
     train(a.warmup)
@@ -137,9 +145,9 @@ def main():
     train(a.steps)
     sync_barrier()
     t1 = time.perf_counter()
-    elapsed = dist_env.allreduce_max(t1 - t0, dev)
+    elapsed = comm_util.all_reduce_scalar(t1 - t0, dist.ReduceOp.MAX)
     ms_per_step = 1e3 * elapsed / a.steps
-    total_samples = dist_env.allreduce_sum(float(per_rank_batch * a.steps), dev)
+    total_samples = comm_util.all_reduce_scalar(float(per_rank_batch * a.steps))
     value = total_samples / elapsed
 
     final_loss = None

@@ -64,6 +64,12 @@ def get_args(argv=None):
                    help="in-repo Trainer: run every batch eagerly instead of replaying it as a hipGraph")
     p.add_argument("--torch_optimizers", action="store_true",
                    help="in-repo Trainer: step the torch optimizers themselves, not the flat-optimizer kernel")
+    p.add_argument("--precision", default="32", choices=["32", "bf16"],
+                   help="32 (the reference's precision=32) or bf16 autocast (fp32 master weights)")
+    p.add_argument("--ckpt_path", default=None,
+                   help="resume: a checkpoint file, or 'last' for the newest one under <root_dir>/lightning_logs")
+    p.add_argument("--every_n_train_steps", type=int, default=0,
+                   help="also save lightning_logs/version_N/checkpoints/last.ckpt every N batches")
     return p.parse_args(argv)
 
 
@@ -83,12 +89,13 @@ def main(argv=None):
             TrainerCls = pl.Trainer
         except ImportError:
             print("pytorch_lightning not installed; using the in-repo Trainer", flush=True)
-    extra = {"seed": a.seed, "use_graphs": not a.no_graphs, "native_optimizers": not a.torch_optimizers} \
-        if TrainerCls is Trainer else {}
-    trainer = TrainerCls(gpus=a.gpus, num_nodes=a.nnodes, max_steps=a.steps, precision=32, accelerator=accel,
+    extra = {"seed": a.seed, "use_graphs": not a.no_graphs, "native_optimizers": not a.torch_optimizers,
+             "every_n_train_steps": a.every_n_train_steps} if TrainerCls is Trainer else {}
+    precision = 32 if a.precision == "32" else "bf16"
+    trainer = TrainerCls(gpus=a.gpus, num_nodes=a.nnodes, max_steps=a.steps, precision=precision, accelerator=accel,
                          log_every_n_steps=min(50, len(dl) / a.batch_size), strategy="ddp",
                          default_root_dir=a.root_dir, enable_progress_bar=not a.no_progress, **extra)
-    trainer.fit(model, dl)
+    trainer.fit(model, dl, ckpt_path=a.ckpt_path)
     if getattr(trainer, "global_rank", 0) == 0:
         sps = None
         if getattr(trainer, "fit_time", None):

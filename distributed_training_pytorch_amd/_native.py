@@ -163,6 +163,7 @@ def _declare(lib):
     P = ctypes.POINTER
     sig = {
         "dtp_version": (c_int, []),
+        "dtp_source_hash": (ctypes.c_char_p, []),
         "dtp_last_error": (ctypes.c_char_p, []),
         "dtp_runtime_last_error": (ctypes.c_char_p, []),
         "dtp_mlp_supported": (c_int, [c_int] * 5),
@@ -236,8 +237,31 @@ def load(build_if_missing: bool = False):
         mine = [ctypes.sizeof(t) for t in (SamplerCfg, Hyper, TrainArgs, StageArgs, OptArgs, GemmArgs)]
         if list(sizes[:6]) != mine:
             raise NativeUnavailable(f"ABI mismatch between libdtp.so {list(sizes[:6])} and _native.py {mine}: rebuild")
+        check_stamp(lib)
         _lib = lib
         return lib
+
+
+def check_stamp(lib) -> None:
+    """The library must have been built from the csrc sources next to it: its baked-in
+    ``dtp_source_hash()`` is compared with ``build.source_hash()`` of the tree (skipped
+    for A/B variant builds loaded through DTP_LIB, and with DTP_SKIP_STAMP=1)."""
+    if os.environ.get("DTP_LIB") or os.environ.get("DTP_SKIP_STAMP") == "1":
+        return
+    from . import build as _build
+
+    if not _build.CSRC.exists():
+        return
+    have = (lib.dtp_source_hash() or b"").decode()
+    want = _build.source_hash()
+    if have != want:
+        raise NativeUnavailable(f"{LIB_PATH} is stale: built from sources {have}, tree has {want}; rebuild with "
+                                "`python -m distributed_training_pytorch_amd.build`")
+
+
+def source_hash() -> str:
+    """Build stamp of the loaded library (``dtp_source_hash``)."""
+    return (load().dtp_source_hash() or b"").decode()
 
 
 def available() -> bool:

@@ -9,6 +9,7 @@ for CDNA4 directly.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -57,23 +58,59 @@ def _headers() -> list[Path]:
     return sorted(CSRC.glob("*.h"))
 
 
-def _stale(target: Path, deps: list[Path]) -> bool:
-    if not target.exists():
-        return True
-    t = target.stat().st_mtime
-    return any(d.stat().st_mtime > t for d in deps)
+def source_hash() -> str:
+    """sha256 (16 hex) over every csrc source and header and the compile flags: the
+    identity of a build.  ``runtime.hip`` bakes it into the library
+    (``dtp_source_hash()``) and ``_native.load()`` refuses a library whose stamp is
+    not the hash of the sources next to it -- so the kernel that ran is tied to the
+    sources of the commit, not to file modification times."""
+    h = hashlib.sha256()
+    for f in sorted([*CSRC.glob("*.hip"), *CSRC.glob("*.h")]):
+        h.update(f.name.encode())
+        h.update(b"\0")
+        h.update(f.read_bytes())
+    h.update(repr((COMMON_FLAGS, sorted(SOURCE_FLAGS.items()))).encode())
+    return h.hexdigest()[:16]
 
 
-def _compile(src: Path, verbose: bool) -> Path:
+def _stamp_ok(target: Path, stamp: str) -> bool:
+    sf = target.with_name(target.name + ".sha")
+    return target.exists() and sf.exists() and sf.read_text().strip() == stamp
+
+
+def _write_stamp(target: Path, stamp: str) -> None:
+    target.with_name(target.name + ".sha").write_text(stamp + "\n")
+
+
+def _obj_stamp(src: Path, full: str) -> str:
+    """An object depends on its source, every header (cheap to over-approximate) and
+    the flags; runtime.hip also on the whole-tree hash it embeds."""
+    h = hashlib.sha256(src.read_bytes())
+    for f in _headers():
+        h.update(f.read_bytes())
+    h.update(repr((COMMON_FLAGS, SOURCE_FLAGS.get(src.name))).encode())
+    if src.name == "runtime.hip":
+        h.update(full.encode())
+    return h.hexdigest()[:16]
+
+
+def _extra_flags(src: Path, full: str) -> list[str]:
+    return [f'-DDTP_SOURCE_HASH="{full}"'] if src.name == "runtime.hip" else []
+
+
+def _compile(src: Path, verbose: bool, full: str) -> Path:
     obj = OBJDIR / (src.stem + ".o")
-    if not _stale(obj, [src, *_headers(), Path(__file__)]):
+    stamp = _obj_stamp(src, full)
+    if _stamp_ok(obj, stamp):
         return obj
-    cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+    cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), *_extra_flags(src, full), "-I", str(CSRC), "-c",
+           str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+    _write_stamp(obj, stamp)
     return obj
 
 
@@ -89,8 +126,8 @@ def variant(name: str, flags: list[str], sources: tuple[str, ...] = ("mlp_train.
     for src in _sources():
         if src.name in sources:
             obj = vdir / "obj" / (src.stem + ".o")
-            cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), *flags, "-I", str(CSRC), "-c", str(src),
-                   "-o", str(obj)]
+            cmd = [hipcc(), *COMMON_FLAGS, *SOURCE_FLAGS.get(src.name, []), *_extra_flags(src, source_hash()),
+                   *flags, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
             if verbose:
                 print(" ".join(cmd), flush=True)
             r = subprocess.run(cmd, capture_output=True, text=True)
@@ -112,9 +149,10 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
     OBJDIR.mkdir(parents=True, exist_ok=True)
     srcs = _sources()
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4) // 2), 8)
+    full = source_hash()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
-    if _stale(LIB, objs):
+        objs = list(ex.map(lambda s: _compile(s, verbose, full), srcs))
+    if not _stamp_ok(LIB, full):
         tmp = LIB.with_suffix(".so.tmp")
         cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
         if verbose:
@@ -123,6 +161,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, LIB)
+        _write_stamp(LIB, full)
     return LIB
 
 

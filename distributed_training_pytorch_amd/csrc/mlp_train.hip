@@ -495,8 +495,10 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   if (disabled || (mode != DTP_MODE_ADAM && mode != DTP_MODE_XGMI_ADAM)) return false;
   const dtp::SamplerCfg& s = a.smp;
   const int ydim = a.loss == DTP_LOSS_CE ? 1 : out;
+  // n >= world: the FAST gather wraps a padded-list position with ONE subtraction of n
+  // (positions stay below n + world - 1), where the generic sampler takes q % n
   return a.cache_data && a.loss == DTP_LOSS_MSE && s.batch <= dtp::kBlock && s.mode == dtp::SAMPLER_DIST_SHUFFLE &&
-         s.bits >= 1 && s.bits < 31 && s.n == (1 << s.bits) && s.n * (in + ydim) <= dtp::kDataCache &&
+         s.bits >= 1 && s.bits < 31 && s.n == (1 << s.bits) && s.n >= s.world && s.n * (in + ydim) <= dtp::kDataCache &&
          a.hp.slope >= 0.f && a.hp.slope <= 1.f;
 }
 

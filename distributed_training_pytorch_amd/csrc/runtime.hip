@@ -49,6 +49,12 @@ int check_launch(const char* what) {
 extern "C" {
 
 int dtp_version(void) { return 1; }
+
+#ifndef DTP_SOURCE_HASH
+#define DTP_SOURCE_HASH "unstamped"
+#endif
+// build stamp: build.py:source_hash() of the sources this library was compiled from
+const char* dtp_source_hash(void) { return DTP_SOURCE_HASH; }
 const char* dtp_last_error(void) { return g_rt_err.c_str(); }
 const char* dtp_runtime_last_error(void) { return g_rt_err.c_str(); }
 

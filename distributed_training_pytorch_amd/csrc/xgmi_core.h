@@ -9,7 +9,8 @@
 //   * a granule is {tag = exchange epoch, two fp32 values, check word}, written
 //     by ONE 16-byte system-scope store; it needs no separate flag or fence: the
 //     consumer polls each granule until its tag equals the epoch it expects and
-//     its check word matches (a torn granule fails the check and is re-polled);
+//     its check word matches (a torn granule fails the check and is re-polled,
+//     up to a 2^-32 collision of the hashed check word);
 //   * PUSH: each rank stores its slot into every peer's buffer (posted xGMI
 //     writes over all 7 links in parallel), then reads only its LOCAL buffer
 //     (its own contribution stays in registers);
@@ -55,8 +56,8 @@ constexpr int kXgmiMaxWorld = 8;
 // as ceil(NPT/2) granules of 16 bytes {epoch, v0, v1, check}; the global mean loss
 // rides in one more granule (thread xgmi_loss_tid).  A granule is written by ONE
 // 16-byte system-scope store and accepted only when its tag equals the expected
-// epoch AND its check word matches the payload, so a reader can never use a torn
-// granule (a 16-byte store landing as two halves fails the check and is re-polled).
+// epoch AND its hashed check word matches the payload, so a torn granule (a 16-byte
+// store landing as two halves) fails the check and is re-polled (2^-32 collisions aside).
 // Half the transactions of one 8-byte {epoch, value} granule per value, and a rank's
 // own contribution never leaves its registers.  (Splitting the workgroup into
 // sender and receiver waves, so no poll waits behind the wave's own remote stores,
@@ -71,8 +72,12 @@ DTP_HD constexpr int xgmi_loss_tid(int P, int nthreads) {
 // granules per (parity, model, source rank) slot, rounded to 64 bytes
 DTP_HD constexpr int xgmi_slot16(int P, int npt) { return (xgmi_nthr(P, npt) * ((npt + 1) / 2) + 1 + 3) & ~3; }
 
+// Check word of a granule: a NONLINEAR mix of tag and payload.  A linear (XOR) check
+// accepts a tear {epoch e, v0 new | v1, check from exchange e-2} whenever
+// v0_new ^ v0_old == e ^ (e-2), a small low-mantissa pattern; through two hash32
+// rounds a tear passes only by a 2^-32 collision.  (A few VALU ops per granule.)
 DTP_DEV uint32_t xgmi_check(uint32_t e, uint32_t a, uint32_t b) {
-  return e ^ a ^ ((b << 13) | (b >> 19)) ^ 0x9E3779B9u;
+  return hash32(e ^ hash32(a ^ ((b << 13) | (b >> 19)) ^ 0x9E3779B9u));
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

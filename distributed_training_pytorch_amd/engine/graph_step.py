@@ -82,6 +82,12 @@ class CapturedStep:
         graph.replay()
         self.replays += 1
 
+    def reset(self) -> None:
+        """Drop every captured graph (the body's launch arguments changed, e.g. new
+        optimizer hyperparameters); the next ``run`` of a key captures it again."""
+        self._graphs.clear()
+        self._seen = {k: self.warmup for k in self._seen}
+
     def is_captured(self, key: Hashable) -> bool:
         g = self._graphs.get(key)
         return g is not None and g is not False

@@ -284,6 +284,10 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
 
     def _flush():
         nonlocal last
+        # ring.flush() syncs with the host anyway: check the sticky xGMI timeout word
+        # here too, so a timed-out exchange stops the run at the next log point instead
+        # of training on partial sums until the end
+        ddp.check_comm()
         for step, (vx, vy) in ring.flush():
             if rank == 0:
                 logger.log({"loss/lossX": vx}, step=step, commit=False)
@@ -329,6 +333,9 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
         if config.checkpoint_dir and config.checkpoint_every and (it + 1) % config.checkpoint_every == 0:
             _flush()
             _save(it + 1)
+            # as in the fused engine: the other ranks wait for rank 0's write on the host
+            # (process-group timeout), not inside the next step's bounded xGMI spin
+            comm_util.barrier()
     _flush()
     if device.type == "cuda":
         torch.cuda.synchronize(device)

@@ -69,8 +69,16 @@ class ToyModel(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
-            if self.uses_fused_kernel():
-                return fused_mlp(x, self.spec, list(self.layers.parameters()))
+            cd = self.compute_dtype
+            if torch.is_autocast_enabled("cuda"):  # autocast (Trainer precision='bf16') picks the compute dtype
+                cd = torch.get_autocast_dtype("cuda")
+            if cd == torch.float32 and self.uses_fused_kernel():
+                return fused_mlp(x.float(), self.spec, list(self.layers.parameters()))
+            if cd == torch.bfloat16 and self.spec.native_supported():
+                # fused stage kernels in bf16 compute: bf16 weights/activations, fp32
+                # accumulation, fp32 master weights and gradients
+                return fused_mlp(x.float(), self.spec, list(self.layers.parameters()), bf16=True)
             lin = [m for m in self.layers if isinstance(m, nn.Linear)]
-            return gemm_mlp(x, [m.weight for m in lin], [m.bias for m in lin], self.spec.slope, self.compute_dtype)
+            with torch.autocast("cuda", enabled=False):
+                return gemm_mlp(x, [m.weight for m in lin], [m.bias for m in lin], self.spec.slope, cd)
         return self.layers(x)

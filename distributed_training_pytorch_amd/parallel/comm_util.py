@@ -52,3 +52,11 @@ def barrier(group=None):
         dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
     else:
         dist.barrier(group=group)
+
+
+def all_reduce_scalar(x: float, op=dist.ReduceOp.SUM, group=None) -> float:
+    """Reduce one host float over the group (f64; a no-op without a process group)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    return float(all_reduce_(t, group, op=op).item())

@@ -28,6 +28,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import _native as nat
+from ..ops.gemm import _fused_grad_target, _grad_ready, mark_fused_grad
 from ..ops.mlp import MlpSpec, mlp_forward_ref, stage_backward, stage_forward
 from . import comm_util
 
@@ -88,9 +89,11 @@ class _PeerStageFn(torch.autograd.Function):
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dst))
             torch.cuda.current_stream(src).wait_event(ev)
-        g = getattr(ctx.param, "grad", None)
-        inplace = (ctx.needs_input_grad[1] and g is not None and g.dtype == torch.float32 and g.is_contiguous()
-                   and g.device == src)
+        # in place only into a persistent flat .grad the owner marked for it
+        # (mark_fused_grad); anything else gets a fresh gradient through autograd,
+        # so torch.autograd.grad and per-parameter hooks behave as usual
+        g = _fused_grad_target(ctx.param) if ctx.needs_input_grad[1] else None
+        inplace = g is not None and g.device == src
         with torch.cuda.device(src):
             gin, gp = stage_backward(x, flat, ctx.spec, out, saved if saved.numel() else None,
                                      grad_out.contiguous(), need_grad_in=ctx.needs_input_grad[0],
@@ -99,8 +102,12 @@ class _PeerStageFn(torch.autograd.Function):
                 ev2 = torch.cuda.Event()
                 ev2.record(torch.cuda.current_stream(src))
                 torch.cuda.current_stream(dst).wait_event(ev2)
-        # in place: the kernel already added into .grad, autograd has nothing to accumulate
-        return gin, (None if inplace else gp), None, None
+        if inplace:
+            # the kernel already added into .grad: autograd has nothing to accumulate,
+            # and the grad-ready hooks (per-stage DDP buckets) fire here instead
+            _grad_ready(ctx.param)
+            return gin, None, None, None
+        return gin, gp, None, None
 
 
 class LayerSplitMLP(nn.Module):
@@ -125,6 +132,7 @@ class LayerSplitMLP(nn.Module):
             self.params.append(nn.Parameter(init_flat[lo:hi].detach().clone().to(dev)))
         for p in self.params:
             p.grad = torch.zeros_like(p)
+            mark_fused_grad(p)  # the stage backward kernel adds into this persistent .grad
         for d0, d1 in zip(self.devices[:-1], self.devices[1:]):
             if d0.type == "cuda" and nat.native_enabled():
                 _enable_peer(d0, d1)

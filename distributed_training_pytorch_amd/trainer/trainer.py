@@ -20,6 +20,7 @@ MI355X-first: a dataset exposing device tensors (``ToyData``) is gathered on the
 """
 from __future__ import annotations
 
+import contextlib
 import csv
 import datetime
 import os
@@ -95,9 +96,16 @@ class Trainer:
                  precision: int = 32, accelerator: str | None = None, strategy: str | None = None,
                  log_every_n_steps: float = 50, default_root_dir: str | None = None,
                  enable_checkpointing: bool = True, enable_progress_bar: bool = True, seed: int | None = None,
-                 use_graphs: bool = True, native_optimizers: bool = True, **unused):
-        if precision not in (32, "32"):
-            raise NotImplementedError("the toy MLP path trains in fp32 (precision=32), like the reference")
+                 use_graphs: bool = True, native_optimizers: bool = True, every_n_train_steps: int = 0,
+                 **unused):
+        if precision in (32, "32", "32-true"):
+            self.autocast_dtype = None
+        elif precision in ("bf16", "bf16-mixed"):
+            # PL: torch.autocast(bf16) around training_step; fp32 master weights and optimizer
+            self.autocast_dtype = torch.bfloat16
+        else:
+            raise NotImplementedError(f"precision={precision!r}: supported are 32 and 'bf16'")
+        self.precision = precision
         self.gpus = gpus
         self.num_nodes = num_nodes
         self.max_steps = max_steps
@@ -118,6 +126,12 @@ class Trainer:
         self.current_epoch = 0
         self.callback_metrics: dict = {}
         self.checkpoint_path: str | None = None
+        # ModelCheckpoint(every_n_train_steps=N): also save ``last.ckpt`` every N batches
+        # (what a restarted job resumes from, fit(ckpt_path="last"))
+        self.every_n_train_steps = int(every_n_train_steps or 0)
+        self._skip_batches = 0
+        self._batch_in_epoch = 0
+        self._log_dir = None
 
     # ------------------------------------------------------------------ distributed
     def _setup(self):
@@ -153,99 +167,184 @@ class Trainer:
         return dl
 
     # ------------------------------------------------------------------ fit
-    def fit(self, model, train_dataloaders=None, train_dataloader=None):
+    def fit(self, model, train_dataloaders=None, train_dataloader=None, ckpt_path: str | None = None):
+        """Train ``model``.  ``ckpt_path`` resumes (PL's ``fit(ckpt_path=...)``): a
+        checkpoint file, or ``"last"`` for the newest ``last.ckpt`` / final checkpoint
+        under ``{root}/lightning_logs``; weights, optimizer states, ``global_step``,
+        epoch and the position inside the epoch are restored, so a restarted job
+        (torchrun ``--max_restarts``) continues where the checkpoint was taken."""
         dl = train_dataloaders if train_dataloaders is not None else train_dataloader
         self._setup()
         if self.seed is not None:
             torch.manual_seed(self.seed)
         model.trainer = self
         model.to(self.device)
+        opts = model.configure_optimizers()
+        if not isinstance(opts, (list, tuple)):
+            opts = [opts]
+        resume = self._resolve_ckpt(ckpt_path)
+        if resume is not None:
+            self._restore(model, opts, resume)
         # the flat gradient buffer of FlatDDP also serves one process: fused kernels add
         # their parameter gradients into its views in place (no AccumulateGrad adds)
         single_ok = self.device.type == "cuda" and all(
             p.dtype == torch.float32 and p.device == self.device for p in model.parameters() if p.requires_grad)
         ddp = FlatDDP(model) if (self.world_size > 1 or single_ok) else None
-        opts = model.configure_optimizers()
-        if not isinstance(opts, (list, tuple)):
-            opts = [opts]
         loader = self._loader(dl)
         self._flat_opts = [_flat_optimizer_for(o, ddp) if self.native_optimizers else None for o in opts]
         stepper, static = self._batch_stepper(model, ddp, opts)
         logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
+        self._log_dir = logger.dir
         pbar = None
         if self.enable_progress_bar and self.global_rank == 0:
             try:
                 from tqdm import tqdm
 
-                pbar = tqdm(total=self.max_steps if self.max_steps > 0 else None, desc="Epoch 0")
+                pbar = tqdm(total=self.max_steps if self.max_steps > 0 else None, desc="Epoch 0",
+                            initial=self.global_step)
             except ImportError:  # pragma: no cover
                 pbar = None
         model.on_train_start()
         t0 = time.perf_counter()
-        done = False
-        while not done:
-            if hasattr(loader, "set_epoch"):
-                loader.set_epoch(self.current_epoch)
-            elif hasattr(getattr(loader, "sampler", None), "set_epoch"):
-                loader.sampler.set_epoch(self.current_epoch)
-            for batch_idx, batch in enumerate(loader):
-                batch = [b.to(self.device, non_blocking=True) for b in batch]
-                if stepper is not None and self._static_ok(static, batch):
-                    key = tuple(tuple(b.shape) for b in batch)
-                    if key not in static:
-                        static[key] = [b.clone() for b in batch]
-                    for dst, src in zip(static[key], batch):
-                        dst.copy_(src)
-                    self._cur_batch_idx = batch_idx  # read by the body only while capturing
-                    replay = stepper.is_captured(key)
-                    stepper.run(key)
-                    # logged tensors of a replay are that key's graph outputs (refreshed in place)
-                    if replay:
-                        model._logged.update(logged_by_key[key])
+        done = 0 < self.max_steps <= self.global_step
+        try:
+            while not done:
+                if hasattr(loader, "set_epoch"):
+                    loader.set_epoch(self.current_epoch)
+                elif hasattr(getattr(loader, "sampler", None), "set_epoch"):
+                    loader.sampler.set_epoch(self.current_epoch)
+                for batch_idx, batch in enumerate(loader):
+                    if batch_idx < self._skip_batches:  # resumed mid-epoch: these already ran
+                        continue
+                    batch = [b.to(self.device, non_blocking=True) for b in batch]
+                    if self._refresh_flat_opts() and stepper is not None:
+                        stepper.reset()  # the captured optimizer launches hold the old hyperparameters
+                    if stepper is not None and self._static_ok(static, batch):
+                        key = tuple(tuple(b.shape) for b in batch)
+                        if key not in static:
+                            static[key] = [b.clone() for b in batch]
+                        for dst, src in zip(static[key], batch):
+                            dst.copy_(src)
+                        self._cur_batch_idx = batch_idx  # read by the body only while capturing
+                        replay = stepper.is_captured(key)
+                        stepper.run(key)
+                        # logged tensors of a replay are that key's graph outputs (refreshed in place)
+                        if replay:
+                            model._logged.update(logged_by_key[key])
+                        else:
+                            logged_by_key[key] = dict(model._logged)
                     else:
-                        logged_by_key[key] = dict(model._logged)
+                        self._optimizer_steps(model, ddp, opts, batch, batch_idx)
+                    self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
+                    self._batch_in_epoch = batch_idx + 1
+                    if self.global_step % self.log_every_n_steps == 0:
+                        metrics = {k: v for k, v in model._logged.items()}
+                        vals = torch.stack([v.float().reshape(()) for v in metrics.values()]).to(self.device)
+                        comm_util.all_reduce_(vals)
+                        vals /= self.world_size
+                        self.callback_metrics = dict(zip(metrics.keys(), vals.tolist()))
+                        logger.log(self.global_step, self.callback_metrics)
+                    if pbar is not None:
+                        pbar.update(1)
+                    if self.every_n_train_steps and self.global_step % self.every_n_train_steps == 0:
+                        self._save(model, opts, "last.ckpt")
+                    if 0 < self.max_steps <= self.global_step:
+                        done = True
+                        break
                 else:
-                    self._optimizer_steps(model, ddp, opts, batch, batch_idx)
-                self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
-                if self.global_step % self.log_every_n_steps == 0:
-                    metrics = {k: v for k, v in model._logged.items()}
-                    vals = torch.stack([v.float().reshape(()) for v in metrics.values()]).to(self.device)
-                    comm_util.all_reduce_(vals)
-                    vals /= self.world_size
-                    self.callback_metrics = dict(zip(metrics.keys(), vals.tolist()))
-                    logger.log(self.global_step, self.callback_metrics)
-                if pbar is not None:
-                    pbar.update(1)
-                if 0 < self.max_steps <= self.global_step:
+                    self.current_epoch += 1
+                    self._batch_in_epoch = 0
+                self._skip_batches = 0
+                if self.max_epochs is not None and self.current_epoch >= self.max_epochs:
                     done = True
-                    break
-            self.current_epoch += 1
-            if self.max_epochs is not None and self.current_epoch >= self.max_epochs:
-                done = True
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
-        self.fit_time = time.perf_counter() - t0
-        if stepper is not None:
-            self.graph_replays = stepper.replays
-        if pbar is not None:
-            pbar.close()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.fit_time = time.perf_counter() - t0
+            if stepper is not None:
+                self.graph_replays = stepper.replays
+        finally:
+            # the user's torch optimizers hold the trained state again -- before any
+            # user hook runs, and also when training raised
+            self._export_flat_opts()
+            if pbar is not None:
+                pbar.close()
         model.on_train_end()
-        for fo in self._flat_opts:
-            if fo is not None:
-                fo.export_state()  # the user's torch optimizers hold the trained state again
-        if self.enable_checkpointing and logger.dir is not None:
-            ck = logger.dir / "checkpoints"
-            ck.mkdir(exist_ok=True)
-            path = ck / f"epoch={self.current_epoch - 1}-step={self.global_step}.ckpt"
-            tmp = path.with_suffix(".tmp")
-            torch.save({"state_dict": {k: v.detach().cpu() for k, v in model.state_dict().items()},
-                        "global_step": self.global_step, "epoch": self.current_epoch - 1,
-                        "optimizer_states": [o.state_dict() for o in opts]}, tmp)
-            os.replace(tmp, path)
-            self.checkpoint_path = str(path)
+        if self.enable_checkpointing:
+            final = f"epoch={max(self.current_epoch - 1, 0) if self._batch_in_epoch == 0 else self.current_epoch}" \
+                    f"-step={self.global_step}.ckpt"
+            self._save(model, opts, final)
         logger.close()
         return self
+
+    # ------------------------------------------------------------------ checkpoints
+    def _ckpt_dir(self) -> Path | None:
+        if self._log_dir is None:
+            return None
+        d = self._log_dir / "checkpoints"
+        d.mkdir(exist_ok=True)
+        return d
+
+    def _save(self, model, opts, name: str) -> None:
+        """Rank-0 atomic save (tmp + rename) of weights, optimizer states and the loop
+        position; every rank then waits for it (a barrier), so no rank can run ahead
+        into a collective while rank 0 is still writing."""
+        self._export_flat_opts()  # torch-format optimizer state of the flat-kernel optimizers
+        d = self._ckpt_dir() if self.global_rank == 0 else None
+        if d is not None:
+            path = d / name
+            tmp = path.with_suffix(".tmp")
+            torch.save({"state_dict": {k: v.detach().cpu() for k, v in model.state_dict().items()},
+                        "global_step": self.global_step, "epoch": self.current_epoch,
+                        "batch_in_epoch": self._batch_in_epoch,
+                        "optimizer_states": [_cpu_state(o.state_dict()) for o in opts]}, tmp)
+            os.replace(tmp, path)
+            self.checkpoint_path = str(path)
+        if dist.is_initialized():
+            comm_util.barrier()
+
+    def _resolve_ckpt(self, ckpt_path):
+        if ckpt_path is None:
+            return None
+        if ckpt_path != "last":
+            return Path(ckpt_path)
+        base = Path(self.root) / "lightning_logs"
+        cands = sorted(base.glob("version_*/checkpoints/*.ckpt"), key=lambda p: p.stat().st_mtime)
+        return cands[-1] if cands else None
+
+    def _restore(self, model, opts, path: Path) -> None:
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        model.load_state_dict(ck["state_dict"])
+        for o, st in zip(opts, ck["optimizer_states"]):
+            o.load_state_dict(st)
+        self.global_step = int(ck["global_step"])
+        self.current_epoch = int(ck["epoch"])
+        self._skip_batches = self._batch_in_epoch = int(ck.get("batch_in_epoch", 0))
+        self.resumed_from = str(path)
+        if self.global_rank == 0:
+            rank_print(0, f"resumed from {path} at global_step {self.global_step}")
+
+    def _refresh_flat_opts(self) -> bool:
+        """Re-read every flat-kernel optimizer's param group (hooks may change lr, ...).
+        True if a hyperparameter changed; an optimizer that left the flat kernel's
+        domain hands its state back to torch and runs torch's own step from now on."""
+        changed = False
+        for i, fo in enumerate(self._flat_opts):
+            if fo is None:
+                continue
+            r = fo.refresh()
+            if r is None:
+                fo.export_state()
+                self._flat_opts[i] = None
+                changed = True
+            else:
+                changed |= r
+        return changed
+
+    def _export_flat_opts(self) -> None:
+        for fo in self._flat_opts:
+            if fo is not None:
+                fo.export_state()
 
     def _optimizer_steps(self, model, ddp, opts, batch, batch_idx):
         """One batch: for each optimizer (PL 1.5): toggle, zero_grad, training_step,
@@ -257,8 +356,9 @@ class Trainer:
                 ddp.zero_grad()
             else:
                 opt.zero_grad(set_to_none=False)
-            out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
-                model.training_step(batch, batch_idx)
+            with self._autocast():
+                out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
+                    model.training_step(batch, batch_idx)
             loss = out["loss"] if isinstance(out, dict) else out
             loss.backward()
             flat = self._flat_opts[oi] if oi < len(self._flat_opts) else None
@@ -269,6 +369,13 @@ class Trainer:
             if len(opts) > 1:
                 model.untoggle_optimizer(oi)
             model._logged[f"train_loss_opt{oi}"] = loss.detach()
+
+    def _autocast(self):
+        """precision='bf16': torch.autocast around the forward (PL's bf16 plugin); the
+        weight-cast cache stays off so a captured hipGraph re-reads the live weights."""
+        if self.autocast_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast(self.device.type, dtype=self.autocast_dtype, cache_enabled=False)
 
     @staticmethod
     def _static_ok(static, batch) -> bool:
@@ -318,13 +425,48 @@ class Trainer:
             dist.destroy_process_group()
 
 
+def _cpu_state(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu()
+    if isinstance(x, dict):
+        return {k: _cpu_state(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_cpu_state(v) for v in x)
+    return x
+
+
+def _optim_config(opt):
+    """OptimConfig of a plain Adam/SGD's single param group, or None if the flat kernel
+    cannot run it (several groups, tensor lr, amsgrad, nesterov, ...)."""
+    from ..ops.optim import OptimConfig
+
+    if len(opt.param_groups) != 1:
+        return None
+    g = opt.param_groups[0]
+    lr = g.get("lr")
+    if isinstance(lr, torch.Tensor) or g.get("maximize") or g.get("differentiable"):
+        return None
+    if type(opt) is torch.optim.Adam:
+        if g.get("amsgrad") or g.get("decoupled_weight_decay"):
+            return None
+        return OptimConfig("adam", float(lr), tuple(float(b) for b in g["betas"]), float(g["eps"]),
+                           float(g["weight_decay"]))
+    if type(opt) is torch.optim.SGD:
+        if g.get("nesterov") or g.get("dampening", 0):
+            return None
+        return OptimConfig("sgd", float(lr), weight_decay=float(g["weight_decay"]), momentum=float(g["momentum"]))
+    return None
+
+
 class _FlatTorchOptimizer:
     """A user's plain ``torch.optim.Adam`` / ``SGD`` run as ONE flat-optimizer kernel
     (``csrc/optim.hip``, the element-for-element mirror of torch's math) over the span
     of the flat parameter buffer its single param group covers, instead of torch's
     ~5 multi-tensor launches plus per-parameter step bookkeeping.  The moments live
-    in flat buffers; ``export_state`` writes them back into ``opt.state`` in torch's
-    own format (checkpoints, continued use of the optimizer)."""
+    in flat buffers (imported from ``opt.state`` when the optimizer was restored from
+    a checkpoint); ``export_state`` writes them back into ``opt.state`` in torch's own
+    format (checkpoints, continued use of the optimizer).  ``refresh`` re-reads the
+    param group, so hyperparameter edits between steps (manual LR decay) apply."""
 
     def __init__(self, opt, params, flat_p, flat_g, cfg):
         from ..ops.optim import FlatOptimizer
@@ -333,6 +475,40 @@ class _FlatTorchOptimizer:
         self.params = params
         self.cfg = cfg
         self.flat = FlatOptimizer(flat_p, flat_g, cfg)
+        self._import_state()
+
+    def _import_state(self):
+        st0 = [self.opt.state.get(p) for p in self.params]
+        if not any(st0):
+            return
+        steps = {int(float(st["step"])) if st and "step" in st else 0 for st in st0}
+        o = 0
+        m, v = self.flat.m.view(-1), self.flat.v.view(-1)
+        with torch.no_grad():
+            for p, st in zip(self.params, st0):
+                n = p.numel()
+                if st:
+                    if self.cfg.name == "adam":
+                        m[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                        v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    elif st.get("momentum_buffer") is not None:
+                        m[o:o + n].copy_(st["momentum_buffer"].reshape(-1))
+                o += n
+        # SGD keeps no step count in torch: a restored momentum buffer means "not the first step"
+        step = max(steps) if self.cfg.name == "adam" else (1 if any(st0) else 0)
+        self.flat.step_ctr.fill_(step)
+        self.opt.state.clear()  # the flat buffers are the live state until export_state
+
+    def refresh(self):
+        """True if the param group's hyperparameters changed (now applied), False if
+        not, None if the optimizer no longer fits the flat kernel."""
+        cfg = _optim_config(self.opt)
+        if cfg is None or cfg.name != self.cfg.name:
+            return None
+        if cfg == self.cfg:
+            return False
+        self.cfg = self.flat.cfg = cfg
+        return True
 
     def step(self):
         self.flat.step()
@@ -361,26 +537,13 @@ def _flat_optimizer_for(opt, ddp):
     """_FlatTorchOptimizer for ``opt`` if it is a plain Adam/SGD whose one param group
     is a contiguous span of the flat buffers on a GPU, else None (torch's step runs)."""
     from ..ops.mlp import _flat_view_of
-    from ..ops.optim import OptimConfig
 
-    if ddp is None or not ddp.flat_params.is_cuda or len(opt.param_groups) != 1 or opt.state:
+    if ddp is None or not ddp.flat_params.is_cuda:
         return None
-    g = opt.param_groups[0]
-    lr = g.get("lr")
-    if isinstance(lr, torch.Tensor) or g.get("maximize") or g.get("differentiable"):
+    cfg = _optim_config(opt)
+    if cfg is None:
         return None
-    if type(opt) is torch.optim.Adam:
-        if g.get("amsgrad") or g.get("decoupled_weight_decay"):
-            return None
-        cfg = OptimConfig("adam", float(lr), tuple(float(b) for b in g["betas"]), float(g["eps"]),
-                          float(g["weight_decay"]))
-    elif type(opt) is torch.optim.SGD:
-        if g.get("nesterov") or g.get("dampening", 0):
-            return None
-        cfg = OptimConfig("sgd", float(lr), weight_decay=float(g["weight_decay"]), momentum=float(g["momentum"]))
-    else:
-        return None
-    params = list(g["params"])
+    params = list(opt.param_groups[0]["params"])
     if not params or any(p.dtype != torch.float32 or p.grad is None for p in params):
         return None
     flat_p = _flat_view_of([p.data for p in params])

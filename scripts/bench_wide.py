@@ -26,7 +26,8 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_training_pytorch_amd.data.toy_data import ToyData  # noqa: E402
-from distributed_training_pytorch_amd.utils import dist_env  # noqa: E402
+from distributed_training_pytorch_amd.parallel import comm_util  # noqa: E402
+from distributed_training_pytorch_amd.runtime import bootstrap  # noqa: E402
 
 
 def run_ours(a, X, Y, dev, world):
@@ -100,22 +101,24 @@ def main():
 
     if a.gemm_backend:
         gemm_mod.set_backend(a.gemm_backend)
-    rank, world, local = dist_env.init_from_env()
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    env = bootstrap.detect()
+    rank, world = env.rank, env.world_size
+    dev = bootstrap.bind_device(env)
+    if world > 1:
+        bootstrap.init_process_group(env, "nccl", dev)
     X, Y = ToyData(n=a.batch * 4, seed=rank).device_tensors(dev)
     for impl in (["ours", "stock"] if a.impl == "both" else [a.impl]):
         step = (run_ours if impl == "ours" else run_stock)(a, X, Y, dev, world)
         for i in range(a.warmup):
             step(i)
         torch.cuda.synchronize()
-        dist_env.barrier()
+        comm_util.barrier()
         t0 = time.perf_counter()
         for i in range(a.steps):
             step(i)
         torch.cuda.synchronize()
-        dist_env.barrier()
-        dt = dist_env.allreduce_max(time.perf_counter() - t0, dev)
+        comm_util.barrier()
+        dt = comm_util.all_reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX)
         params = 2 * (2 * a.width + a.width + a.depth * (a.width * a.width + a.width) + a.width + 1)
         flops = 6.0 * params * a.batch * a.steps * world  # fwd + bwd (dx, dW) of both models
         if rank == 0:

@@ -18,18 +18,19 @@ from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, 
 from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC  # noqa: E402
 from distributed_training_pytorch_amd.parallel.xgmi import DeviceBarrier  # noqa: E402
-from distributed_training_pytorch_amd.utils import dist_env  # noqa: E402
+from distributed_training_pytorch_amd.runtime import bootstrap  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--reps", type=int, default=6)
 a = ap.parse_args()
 _native.set_wait_mode(os.environ.get("DTP_WAIT_MODE", "spin"))
-os.environ["LOCAL_RANK"] = "0"
-rank, world, _ = dist_env.init_from_env(backend="gloo")
-dev = torch.device("cuda", 0)
-torch.cuda.set_device(dev)
-n = 512 * world
+env = bootstrap.detect()
+env.local_rank = 0
+rank, world = env.rank, env.world_size
+dev = bootstrap.bind_device(env)
+bootstrap.init_process_group(env, "gloo", dev)
+n = 512
 X, Y = ToyData(n=n, seed=0).device_tensors(dev)
 geom = SamplerGeometry(n=n, world=world, rank=rank, batch=256, seed=0)
 torch.manual_seed(0)

@@ -1,0 +1,42 @@
+"""Ground-truth training loop for the loss / optimizer options: plain autograd +
+``torch.optim`` (not the repo's own reference helpers), data-parallel semantics
+(the step's gradient is the mean of the per-rank batch gradients, the logged loss
+the mean of the per-rank losses)."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from distributed_training_pytorch_amd.ops.mlp import mlp_forward_ref
+from distributed_training_pytorch_amd.ops.optim import OptimConfig
+
+
+def loss_fn(out, y, loss: str):
+    if loss == "ce":
+        return F.cross_entropy(out, y.view(-1).long())
+    return F.mse_loss(out, y.view_as(out))
+
+
+def torch_train(spec, init, X, Y, geoms, steps: int, ocfg: OptimConfig, loss: str = "mse"):
+    """init: list of [P] tensors (one per model); geoms: one SamplerGeometry (or any
+    object with .indices(t)) per rank.  Returns (params [n_models, P], losses [steps, n_models])."""
+    X, Y = X.detach().cpu().double(), Y.detach().cpu()
+    params = [torch.nn.Parameter(p.detach().cpu().double().clone()) for p in init]
+    opts = [ocfg.torch_optimizer([p]) for p in params]
+    losses = []
+    for t in range(steps):
+        row = []
+        for p, opt in zip(params, opts):
+            gs, ls = [], []
+            for g in geoms:
+                idx = torch.tensor(g.indices(t), dtype=torch.long)
+                q = p.detach().clone().requires_grad_(True)
+                lo = loss_fn(mlp_forward_ref(q, spec, X[idx]), Y[idx].double() if loss == "mse" else Y[idx], loss)
+                (gr,) = torch.autograd.grad(lo, q)
+                gs.append(gr)
+                ls.append(lo.item())
+            p.grad = torch.stack(gs).mean(0)
+            opt.step()
+            row.append(sum(ls) / len(geoms))
+        losses.append(row)
+    return torch.stack([p.detach().float() for p in params]), torch.tensor(losses, dtype=torch.float32)

@@ -37,18 +37,69 @@ def test_bench_one_gpu_json_contract():
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec, k
     assert rec["n_gpus"] == 1 and rec["steps"] == 200 and rec["value"] > 1e6
-    assert rec["config"]["parallelism"] == "dp1"
+    assert rec["config"]["parallelism"] == "dp1" and rec["scaling"] == "strong"
+    assert rec["config"]["global_batch"] == 256 and rec["config"]["dataset_samples"] == 512
 
 
-def test_bench_two_ranks_share_gpu():
+def _single_process_full_batch_losses(steps: int) -> list[float]:
+    """The strong-scaling reference: at W >= 2 the 512-sample set is split over the W
+    ranks with per-rank batch 512/W, so one step of the job sees every sample once --
+    the same update as ONE process training on batch 512 (summation order aside)."""
+    import torch
+
+    sys.path.insert(0, ROOT)
+    from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+    from distributed_training_pytorch_amd.data.toy_data import ToyData
+    from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
+    from distributed_training_pytorch_amd.models.toy import ToyModel
+    from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
+    from distributed_training_pytorch_amd.ops.optim import OptimConfig
+
+    dev = torch.device("cuda", 0)
+    X, Y = ToyData(n=512, seed=0).device_tensors(dev)
+    torch.manual_seed(0)
+    init = [ToyModel().flat_params.detach().clone() for _ in range(2)]
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=512, seed=0), OptimConfig(lr=1e-3),
+                      EngineConfig(steps_per_launch=64), init_params=init)
+    tr.train(steps)
+    tr.synchronize()
+    out = tr.losses(steps - 1, steps)[0].tolist()
+    tr.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_strong_scaling_share_gpu(world):
+    """The driver's N-GPU bench config, rehearsed with W ranks on the one GPU: the
+    reference's strong-scaling workload (512 samples total, per-rank batch 512/W),
+    in-kernel xGMI exchange, and the final global loss of the job equal to one
+    process training the full 512-sample batch."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    steps, warmup = 60, 20
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world),
+           "--share-gpu", "--steps", str(steps), "--warmup", str(warmup)]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["scaling"] == "strong"
+    assert rec["n_gpus"] == world and rec["config"]["parallelism"] == f"dp{world}"
+    assert rec["config"]["comm"] == "xgmi", rec["config"]
+    assert rec["config"]["dataset_samples"] == 512
+    assert rec["config"]["global_batch"] == 512
+    assert rec["config"]["per_rank_batch"] == 512 // world
+    ref = _single_process_full_batch_losses(steps + warmup)
+    for got, want in zip(rec["final_loss"], ref):
+        assert abs(got - want) <= 1e-3 * abs(want) + 1e-5, (rec["final_loss"], ref)
+
+
+def test_bench_weak_scaling_flag_share_gpu():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--share-gpu",
-           "--steps", "200", "--warmup", "20"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+           "--scaling", "weak", "--steps", "100", "--warmup", "10"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
-    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
-    assert rec["config"]["comm"] == "xgmi", rec["config"]
-    assert rec["config"]["global_batch"] == 512
-    assert all(abs(v) < 10 for v in rec["final_loss"])
+    assert rec["scaling"] == "weak" and rec["config"]["global_batch"] == 512
+    assert rec["config"]["per_rank_batch"] == 256 and rec["config"]["dataset_samples"] == 1024

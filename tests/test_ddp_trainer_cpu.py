@@ -125,3 +125,35 @@ def test_flatddp_in_place_gemm_grads_match_torch_ddp():
         assert nb > 1
         torch.testing.assert_close(g, gref, rtol=1e-5, atol=1e-6)
     assert torch.equal(res[0][0], res[1][0])
+
+
+def _lit_run(tmp_path, steps, ckpt_path=None, every=0, precision=32):
+    sys.path.insert(0, str(ROOT))
+    from demo_pytorch_lightning import LitToyModel
+    from distributed_training_pytorch_amd.data.toy_data import ToyData
+    from distributed_training_pytorch_amd.trainer import Trainer
+
+    torch.manual_seed(0)
+    ds = ToyData(seed=0)
+    dl = torch.utils.data.DataLoader(ds, batch_size=128)
+    model = LitToyModel()
+    tr = Trainer(gpus=0, max_steps=steps, accelerator="cpu", log_every_n_steps=1, default_root_dir=str(tmp_path),
+                 enable_progress_bar=False, every_n_train_steps=every, precision=precision)
+    tr.fit(model, dl, ckpt_path=ckpt_path)
+    return tr, model
+
+
+def test_trainer_resume_is_bit_exact(tmp_path):
+    """fit(ckpt_path="last") continues a run from its periodic last.ckpt (weights, both
+    Adams, global_step, epoch and the position inside the epoch: 512 samples / batch
+    128 = 4 batches per epoch, so step 6 is mid-epoch) and ends bitwise where an
+    uninterrupted run ends."""
+    ref_tr, ref = _lit_run(tmp_path / "ref", 10)
+    a_tr, _ = _lit_run(tmp_path / "run", 6, every=3)
+    assert (tmp_path / "run" / "lightning_logs" / "version_0" / "checkpoints" / "last.ckpt").exists()
+    b_tr, b = _lit_run(tmp_path / "run", 10, ckpt_path="last")
+    assert b_tr.resumed_from.endswith(".ckpt")
+    assert b_tr.global_step == 10 == ref_tr.global_step
+    assert b_tr.current_epoch == ref_tr.current_epoch
+    for (k, v), (k2, v2) in zip(ref.state_dict().items(), b.state_dict().items()):
+        assert k == k2 and torch.equal(v, v2), k

@@ -111,3 +111,42 @@ def test_device_barrier_falls_back_to_the_process_group():
     res = run_ranks(_barrier_fn, 2, ())
     assert res[0][1] is False and res[1][1] is False
     assert res[0][0] > 0.2  # rank 0 waited for the late rank
+
+
+def _loss_optim_rank(rank, world, loss, ocfg, steps):
+    from distributed_training_pytorch_amd.ops.mlp import MlpSpec
+
+    spec = MlpSpec(2, 10, 5, 4) if loss == "ce" else TOY_SPEC
+    ds = ToyData(n=512, seed=3, classes=4 if loss == "ce" else 0)
+    geom = SamplerGeometry(n=512, world=world, rank=rank, batch=128, seed=11)
+    g = torch.Generator().manual_seed(100)
+    init = [torch.randn(spec.P, generator=g) * 0.4 for _ in range(2)]
+    tr = FusedTrainer(spec, 2, ds.X, ds.Y, geom, ocfg, EngineConfig(loss=loss), init_params=init)
+    tr.train(steps)
+    return tr.params.clone(), tr.losses(0, steps)
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("loss,ocfg", [("ce", OptimConfig(lr=1e-2)),
+                                       ("mse", OptimConfig("sgd", 5e-2, momentum=0.9, weight_decay=1e-4)),
+                                       ("ce", OptimConfig("sgd", 5e-2, momentum=0.9))])
+def test_loss_and_optimizer_options_gloo_dp(loss, ocfg):
+    """--loss ce / --optimizer sgd on the CPU (gloo, 2 ranks) path against autograd +
+    torch.optim (F.cross_entropy, torch.optim.SGD with momentum / weight decay)."""
+    from distributed_training_pytorch_amd.ops.mlp import MlpSpec
+
+    from .ref_train import torch_train
+
+    steps = 8
+    res = run_ranks(_loss_optim_rank, 2, (loss, ocfg, steps))
+    spec = MlpSpec(2, 10, 5, 4) if loss == "ce" else TOY_SPEC
+    ds = ToyData(n=512, seed=3, classes=4 if loss == "ce" else 0)
+    geoms = [SamplerGeometry(n=512, world=2, rank=r, batch=128, seed=11) for r in range(2)]
+    g = torch.Generator().manual_seed(100)
+    init = [torch.randn(spec.P, generator=g) * 0.4 for _ in range(2)]
+    rp, rl = torch_train(spec, init, ds.X, ds.Y, geoms, steps, ocfg, loss)
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][0], rp, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(res[0][1], rl, rtol=1e-5, atol=1e-6)

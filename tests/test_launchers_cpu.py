@@ -193,3 +193,18 @@ def test_resume_is_bit_exact(tmp_path, engine):
         assert torch.equal(a["params"], b["params"])
         for k in ("m", "v", "step"):
             assert torch.equal(a["optim_state"][k], b["optim_state"][k]), k
+
+
+@pytest.mark.parametrize("engine", ["fused", "module"])
+def test_demo_cross_entropy_sgd_two_ranks(engine):
+    """demo.py --loss ce --optimizer sgd under torchrun with gloo: both engines train and
+    agree with each other (same sampler order, same math)."""
+    outs = {}
+    for eng in (engine,):
+        r = _run([PY, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--master-addr",
+                  "127.0.0.1", "--master-port", str(_free_port()), "demo.py", "--torchrun", *COMMON,
+                  "--engine", eng, "--loss", "ce", "--optimizer", "sgd", "--lr", "0.05", "--momentum", "0.9"])
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs[eng] = _summary(r.stdout)
+    s = outs[engine]
+    assert s["iters"] == 20 and all(0.0 < v < 5.0 for v in s["final_loss"])
