@@ -37,8 +37,9 @@ def build_parser(description: str | None = None) -> argparse.ArgumentParser:
     p.add_argument("--hidden", type=int, default=10)
     p.add_argument("--depth", type=int, default=3, help="number of hidden Linear(h,h) layers")
     p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
-                   help="fp32 = the reference (precision=32); bf16 = bf16 GEMM compute with fp32 master weights "
-                        "(wide models on the MFMA GEMM path; the fused toy kernel is fp32 only)")
+                   help="fp32 = the reference (precision=32); bf16 = bf16 matmul operands with fp32 "
+                        "accumulation, fp32 master weights and optimizer (fused toy kernels have bf16 "
+                        "instances; wide models run bf16 on the MFMA GEMM path)")
     p.add_argument("--timeout_min", type=float, default=60.0, help="process-group timeout (demo.py:27)")
     # --- MI355X engine ---------------------------------------------------------
     p.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto")

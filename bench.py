@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32 = the reference's precision=32 (the headline); bf16 = bf16 matmul operands, "
+                         "fp32 accumulation / master weights / Adam (BASELINE config 2)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:(local_rank %% device_count), gloo process group "
@@ -109,7 +112,8 @@ def main():
         geom = SamplerGeometry(n=n, world=world, rank=rank, batch=a.batch, seed=a.seed)
         torch.manual_seed(a.seed)
         init = [ToyModel().flat_params.detach().clone() for _ in range(2)]
-        ecfg = EngineConfig(comm=a.comm, launch=a.launch, steps_per_launch=a.steps_per_launch)
+        ecfg = EngineConfig(comm=a.comm, launch=a.launch, steps_per_launch=a.steps_per_launch,
+                            precision=a.precision)
         runner = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
         per_rank_batch = geom.batch_size_at(0)
         train = runner.train
@@ -176,7 +180,7 @@ def main():
             "higher_is_better": True,
             "scaling": a.scaling,
             "vs_baseline": (value / base) if (base and a.impl == "native") else None,
-            "dtype": "fp32",
+            "dtype": a.precision if a.impl == "native" else "fp32",
             "data": "synthetic (ToyData distribution, seeded; random-init ToyModel weights)",
             "config": {
                 "model": "2x ToyModel MLP 2-10-10-10-10-1 LeakyReLU (X,Y), MSE, Adam lr=1e-3",

@@ -81,6 +81,8 @@ class TrainArgs(ctypes.Structure):
         ("loss", c_int),
         ("cache_data", c_int),
         ("timeout_us", c_int),
+        ("bf16", c_int),
+        ("pad_", c_int),
         ("smp", SamplerCfg),
         ("hp", Hyper),
     ]
@@ -99,6 +101,47 @@ class StageArgs(ctypes.Structure):
         ("batch", c_int),
         ("slope", c_float),
         ("accumulate", c_int),
+        ("bf16", c_int),
+    ]
+
+
+class SplitStageArgs(ctypes.Structure):
+    _fields_ = [
+        ("X", c_void_p),
+        ("Y", c_void_p),
+        ("params", c_void_p),
+        ("opt_m", c_void_p),
+        ("opt_v", c_void_p),
+        ("step", c_void_p),
+        ("loss_log", c_void_p),
+        ("status", c_void_p),
+        ("act_in", c_void_p),
+        ("act_out", c_void_p),
+        ("grad_in", c_void_p),
+        ("grad_out", c_void_p),
+        ("dp_peers", c_void_p),
+        ("loss_log_cap", c_int),
+        ("n_steps", c_int),
+        ("timeout_us", c_int),
+        ("cache_data", c_int),
+        ("dp_world", c_int),
+        ("dp_rank", c_int),
+        ("optim", c_int),
+        ("pad_", c_int),
+        ("smp", SamplerCfg),
+        ("hp", Hyper),
+    ]
+
+
+SPLIT_MAX_LOCAL = 8
+
+
+class SplitLaunch(ctypes.Structure):
+    _fields_ = [
+        ("stage", SplitStageArgs * SPLIT_MAX_LOCAL),
+        ("shape_id", c_int * SPLIT_MAX_LOCAL),
+        ("n", c_int),
+        ("pad_", c_int),
     ]
 
 
@@ -167,8 +210,10 @@ def _declare(lib):
         "dtp_last_error": (ctypes.c_char_p, []),
         "dtp_runtime_last_error": (ctypes.c_char_p, []),
         "dtp_mlp_supported": (c_int, [c_int] * 5),
+        "dtp_mlp_supported_bf16": (c_int, [c_int] * 5),
         "dtp_mlp_param_count": (c_int, [c_int] * 4),
         "dtp_mlp_workspace_floats": (c_int, [c_int] * 4),
+        "dtp_mlp_train_bf16_supported": (c_int, [c_int] * 4),
         "dtp_mlp_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
         "dtp_xgmi_fused_buffer_bytes": (c_longlong, [c_int, c_int, c_int]),
@@ -178,6 +223,10 @@ def _declare(lib):
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
+        "dtp_split_launch": (c_int, [P(SplitLaunch), c_void_p]),
+        "dtp_split_shape_id": (c_int, [c_int] * 6),
+        "dtp_split_stage_supported": (c_int, [c_int] * 6),
+        "dtp_split_link_bytes": (c_longlong, [c_int, c_int]),
         "dtp_sampler_indices": (c_int, [P(SamplerCfg), c_longlong, c_int, c_void_p, c_void_p]),
         "dtp_get_device": (c_int, [P(c_int)]),
         "dtp_device_count": (c_int, [P(c_int)]),
@@ -201,8 +250,9 @@ def _declare(lib):
         "dtp_graph_destroy": (c_int, [c_void_p]),
         "dtp_struct_sizes": (c_int, [P(c_int)]),
         "dtp_gemm": (c_int, [P(GemmArgs), c_void_p]),
-        "dtp_xgmi_allreduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, ctypes.c_uint, c_float,
+        "dtp_xgmi_allreduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_float,
                                        c_void_p, c_int, c_void_p]),
+        "dtp_xgmi_allreduce_epoch_slots": (c_int, [c_int]),
         "dtp_colsum": (c_int, [c_void_p, c_longlong, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
@@ -234,9 +284,10 @@ def load(build_if_missing: bool = False):
         _declare(lib)
         sizes = (c_int * 8)()
         lib.dtp_struct_sizes(sizes)
-        mine = [ctypes.sizeof(t) for t in (SamplerCfg, Hyper, TrainArgs, StageArgs, OptArgs, GemmArgs)]
-        if list(sizes[:6]) != mine:
-            raise NativeUnavailable(f"ABI mismatch between libdtp.so {list(sizes[:6])} and _native.py {mine}: rebuild")
+        mine = [ctypes.sizeof(t) for t in (SamplerCfg, Hyper, TrainArgs, StageArgs, OptArgs, GemmArgs, SplitStageArgs,
+                                            SplitLaunch)]
+        if list(sizes[:8]) != mine:
+            raise NativeUnavailable(f"ABI mismatch between libdtp.so {list(sizes[:8])} and _native.py {mine}: rebuild")
         check_stamp(lib)
         _lib = lib
         return lib

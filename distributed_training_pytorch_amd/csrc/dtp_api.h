@@ -43,6 +43,8 @@ struct DtpTrainArgs {
   int loss;             // DtpLoss
   int cache_data;       // stage the dataset in LDS (persistent multi-step runs)
   int timeout_us;       // bound on every cross-GPU spin (xGMI)
+  int bf16;             // bf16 compute instance (fp32 master weights / Adam), toy shapes
+  int pad_;
   dtp::SamplerCfg smp;
   DtpHyper hp;
 };
@@ -50,8 +52,10 @@ struct DtpTrainArgs {
 int dtp_version(void);
 const char* dtp_last_error(void);
 int dtp_mlp_supported(int in, int h, int nl, int out, int final_act);
+int dtp_mlp_supported_bf16(int in, int h, int nl, int out, int final_act);
 int dtp_mlp_param_count(int in, int h, int nl, int out);
 int dtp_mlp_workspace_floats(int in, int h, int nl, int out);
+int dtp_mlp_train_bf16_supported(int in, int h, int nl, int out);
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream);
 int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream);
 long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world);
@@ -70,10 +74,58 @@ struct DtpStageArgs {
   int batch;
   float slope;
   int accumulate;  // backward: add into grad_params (a persistent .grad view) instead of overwriting it
+  int bf16;        // bf16 compute (Stage<..., BF>: bf16 operands, fp32 accumulation and weight gradients)
 };
 
 int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);
 int dtp_mlp_stage_bwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);
+
+// ---- persistent layer-split pipeline stage (split_train.hip) ----
+// One stage of a model split by layers over several GPUs, resident for n_steps
+// iterations: the stage's activation goes to the next stage and the input gradient
+// back to the previous one as epoch-tagged granules stored straight into the
+// neighbour GPU's receive buffer (peer-mapped over xGMI); the stage's weight
+// gradient is (optionally) all-reduced over the data-parallel ranks in-kernel and
+// the optimizer is fused.
+struct DtpSplitStageArgs {
+  const float* X;         // [n][IN of the model]  dataset inputs (first stage)
+  const float* Y;         // [n][OUT of the model] targets (last stage)
+  float* params;          // [P] this stage's parameters (torch order)
+  float* opt_m;           // [P] Adam exp_avg / SGD momentum
+  float* opt_v;           // [P] Adam exp_avg_sq
+  int* step;              // [1] optimizer step counter (device)
+  float* loss_log;        // [loss_log_cap] global mean loss per step (last stage), nullable
+  int* status;            // [16]: [0,1] stage-link timeout flag / epoch, [2,3] data-parallel exchange
+  void* act_in;           // receive buffer of the incoming activation (not the first stage), local
+  void* act_out;          // the next stage's act_in, peer-mapped (not the last stage)
+  void* grad_in;          // receive buffer of the incoming output gradient (not the last stage), local
+  void* grad_out;         // the previous stage's grad_in, peer-mapped (not the first stage)
+  float* const* dp_peers; // [dp_world] this stage's exchange buffers on every DP rank (dp_world > 1)
+  int loss_log_cap;
+  int n_steps;
+  int timeout_us;
+  int cache_data;
+  int dp_world;
+  int dp_rank;
+  int optim;              // DTP_MODE_ADAM or DTP_MODE_SGD
+  int pad_;
+  dtp::SamplerCfg smp;
+  DtpHyper hp;            // grad_scale = 1 / dp_world
+};
+
+#define DTP_SPLIT_MAX_LOCAL 8
+// the stages placed on one GPU, launched together (one workgroup each)
+struct DtpSplitLaunch {
+  DtpSplitStageArgs stage[DTP_SPLIT_MAX_LOCAL];
+  int shape_id[DTP_SPLIT_MAX_LOCAL];  // dtp_split_shape_id of each stage
+  int n;
+  int pad_;
+};
+
+int dtp_split_launch(const DtpSplitLaunch* L, void* stream);
+int dtp_split_shape_id(int in, int h, int nl, int out, int final_act, int first);
+long long dtp_split_link_bytes(int width, int batch);
+int dtp_split_stage_supported(int in, int h, int nl, int out, int final_act, int first);
 
 // ---- flat optimizers over [n_models][P] (after an external all-reduce) ----
 struct DtpOptArgs {

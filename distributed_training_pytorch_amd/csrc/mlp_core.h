@@ -20,10 +20,23 @@ namespace dtp {
 // A stage = NL Linear layers  IN -> H -> ... -> H -> OUT, LeakyReLU after every
 // layer but the last (and after the last too when FINAL_ACT, which is how a
 // layer-split stage that ends inside the network looks).
-template <int IN_, int H_, int NL_, int OUT_, bool FINAL_ACT_>
+// BF: bf16 compute (the autocast recipe): every matmul operand -- weights,
+// activations, backward gradients -- is rounded to bf16 (rnd), products are exact in
+// fp32 and accumulate in fp32 (FMA chains and the fp32 MFMA dW tiles: the numerics of
+// a bf16 MFMA with fp32 accumulation); master weights, weight gradients and the
+// optimizer stay fp32.  BF = false compiles every rnd() away.
+template <int IN_, int H_, int NL_, int OUT_, bool FINAL_ACT_, bool BF_ = false>
 struct Stage {
   static constexpr int IN = IN_, H = H_, NL = NL_, OUT = OUT_;
   static constexpr bool FINAL_ACT = FINAL_ACT_;
+  static constexpr bool BF = BF_;
+  static DTP_DEV float rnd(float v) {
+    if constexpr (BF) {
+      return (float)(__bf16)v;  // v_cvt_pk_bf16_f32: round to nearest even
+    } else {
+      return v;
+    }
+  }
   static constexpr int din(int l) { return l == 0 ? IN : H; }
   static constexpr int dout(int l) { return l == NL - 1 ? OUT : H; }
   static constexpr bool act(int l) { return l < NL - 1 ? true : FINAL_ACT; }
@@ -94,6 +107,7 @@ DTP_DEV int lds_pos_t(int p) {
 // stage parameter p (torch order) into both LDS copies
 template <class S>
 DTP_DEV void lds_store_param(float* __restrict__ sw, int p, float v) {
+  v = S::rnd(v);  // bf16 compute: the matmul operand is the bf16 weight
   sw[lds_pos<S>(p)] = v;
   const int t = lds_pos_t<S>(p);
   if (t >= 0) sw[t] = v;
@@ -157,9 +171,9 @@ DTP_DEV void mlp_forward(const float* __restrict__ sw, float (&h)[S::NL + 1][16]
     static_for<0, O>([&](auto JC) {
       constexpr int j = decltype(JC)::value;
       if constexpr (S::act(l)) {
-        h[l + 1][j] = leaky(z[j], slope);
+        h[l + 1][j] = S::rnd(leaky(S::rnd(z[j]), slope));  // bf16 Linear output, then bf16 LeakyReLU
       } else {
-        h[l + 1][j] = z[j];
+        h[l + 1][j] = S::rnd(z[j]);
       }
     });
   });
@@ -260,10 +274,10 @@ DTP_DEV void mlp_backward(const float* __restrict__ sw, const float (&h)[S::NL +
       if constexpr (l > 0) {
         static_for<0, I>([&](auto IC) {
           constexpr int i = decltype(IC)::value;
-          dz[i] = g[i] * (S::act(l - 1) ? leaky_grad_from_out(h[l][i], slope) : 1.f);
+          dz[i] = S::rnd(S::rnd(g[i]) * (S::act(l - 1) ? leaky_grad_from_out(h[l][i], slope) : 1.f));
         });
       } else {
-        static_for<0, I>([&](auto IC) { dx[decltype(IC)::value] = g[decltype(IC)::value]; });
+        static_for<0, I>([&](auto IC) { dx[decltype(IC)::value] = S::rnd(g[decltype(IC)::value]); });
       }
     }
     __builtin_amdgcn_wave_barrier();

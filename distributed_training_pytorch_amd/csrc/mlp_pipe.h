@@ -116,8 +116,8 @@ DTP_DEV void pipe_fwd_layer(const float* __restrict__ wl, const FBlk<S, l>& B, f
   });
   static_for<0, O>([&](auto JC) {
     constexpr int j = decltype(JC)::value;
-    const float v = (j & 1) ? z[j / 2].y : z[j / 2].x;
-    h[l + 1][j] = S::act(l) ? (LM ? fmaxf(v, v * slope) : leaky(v, slope)) : v;
+    const float v = S::rnd((j & 1) ? z[j / 2].y : z[j / 2].x);  // bf16: the Linear output, then the activation
+    h[l + 1][j] = S::rnd(S::act(l) ? (LM ? fmaxf(v, v * slope) : leaky(v, slope)) : v);
   });
 }
 
@@ -203,7 +203,7 @@ DTP_DEV void pipe_bwd_layer(const PipeBwdCtx<S>& c, const BBlk<S, l>& B, const f
   static_for<0, I>([&](auto IC) {
     constexpr int i = decltype(IC)::value;
     const float v = (i & 1) ? g[i / 2].y : g[i / 2].x;
-    dz[i] = v * (S::act(l - 1) ? leaky_grad_from_out(h[l][i], c.slope) : 1.f);
+    dz[i] = S::rnd(S::rnd(v) * (S::act(l - 1) ? leaky_grad_from_out(h[l][i], c.slope) : 1.f));
   });
 }
 

@@ -149,7 +149,7 @@ DTP_DEV void lds_forward(const float* __restrict__ wl, float (&h)[S::NL + 1][16]
     static_for<0, O>([&](auto JC) {
       constexpr int j = decltype(JC)::value;
       const float v = (j & 1) ? z[j / 2].y : z[j / 2].x;
-      h[l + 1][j] = S::act(l) ? leaky(v, slope) : v;
+      h[l + 1][j] = S::rnd(S::act(l) ? leaky(S::rnd(v), slope) : v);
     });
   });
 }
@@ -201,7 +201,7 @@ DTP_DEV void lds_backward_dx(const float* __restrict__ wl, const float (&h)[S::N
   static_for<0, I>([&](auto IC) {
     constexpr int i = decltype(IC)::value;
     const float v = (i & 1) ? g[i / 2].y : g[i / 2].x;
-    dz[i] = v * (S::act(l - 1) ? leaky_grad_from_out(h[l][i], slope) : 1.f);
+    dz[i] = S::rnd(S::rnd(v) * (S::act(l - 1) ? leaky_grad_from_out(h[l][i], slope) : 1.f));
   });
 }
 

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_fwd_kernel(DtpStageArgs a) {
   const int b = blockIdx.x * kBlock + threadIdx.x;
   if (b >= a.batch) return;
   float h[S::NL + 1][16];
-  static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = a.x[(size_t)b * S::IN + decltype(IC)::value]; });
+  static_for<0, S::IN>([&](auto IC) { h[0][decltype(IC)::value] = S::rnd(a.x[(size_t)b * S::IN + decltype(IC)::value]); });
   mlp_forward<S>(sw, h, a.slope);
   static_for<0, S::OUT>([&](auto JC) { a.out[(size_t)b * S::OUT + decltype(JC)::value] = h[S::NL][decltype(JC)::value]; });
   if (a.out_peer) {  // layer-split hand-off: the epilogue writes the next GPU's input directly
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
     float h[S::NL + 1][16];
     static_for<0, S::IN>([&](auto IC) {
       constexpr int i = decltype(IC)::value;
-      h[0][i] = valid ? a.x[(size_t)b * S::IN + i] : 0.f;
+      h[0][i] = valid ? S::rnd(a.x[(size_t)b * S::IN + i]) : 0.f;
     });
     static_for<1, S::NL>([&](auto LC) {
       constexpr int l = decltype(LC)::value;
@@ -71,8 +71,8 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
     float dz[16];
     static_for<0, S::OUT>([&](auto JC) {
       constexpr int j = decltype(JC)::value;
-      float go = valid ? a.grad_out[(size_t)b * S::OUT + j] : 0.f;
-      if constexpr (S::FINAL_ACT) go *= leaky_grad_from_out(valid ? a.out[(size_t)b * S::OUT + j] : 0.f, a.slope);
+      float go = valid ? S::rnd(a.grad_out[(size_t)b * S::OUT + j]) : 0.f;
+      if constexpr (S::FINAL_ACT) go = S::rnd(go * leaky_grad_from_out(valid ? a.out[(size_t)b * S::OUT + j] : 0.f, a.slope));
       dz[j] = go;
     });
     float dx[16];
@@ -125,6 +125,11 @@ using dtp::set_err;
   X(2, 15, 5, 4, false)     \
   X(4, 15, 5, 4, false)
 
+// whole-model shapes that also have bf16-compute instances (autocast / precision='bf16')
+#define DTP_STAGE_BF16_SHAPES(X) \
+  X(2, 10, 5, 1, false)          \
+  X(2, 10, 5, 4, false)
+
 template <class S>
 int launch_stage_fwd(const DtpStageArgs* a, hipStream_t st) {
   if (a->batch <= 0) return 0;
@@ -151,6 +156,14 @@ int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
 
 extern "C" {
 
+int dtp_mlp_supported_bf16(int in, int h, int nl, int out, int final_act) {
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return 1;
+  DTP_STAGE_BF16_SHAPES(X)
+#undef X
+  return 0;
+}
+
 int dtp_mlp_supported(int in, int h, int nl, int out, int final_act) {
 #define X(I, H, N, O, F) \
   if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return 1;
@@ -161,6 +174,13 @@ int dtp_mlp_supported(int in, int h, int nl, int out, int final_act) {
 
 int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (a->bf16) {
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_fwd<dtp::Stage<I, H, N, O, F, true>>(a, st);
+    DTP_STAGE_BF16_SHAPES(X)
+#undef X
+    return set_err(-2, "no bf16 instance of this mlp stage shape");
+  }
 #define X(I, H, N, O, F) \
   if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_fwd<dtp::Stage<I, H, N, O, F>>(a, st);
   DTP_STAGE_SHAPES(X)
@@ -170,6 +190,13 @@ int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int
 
 int dtp_mlp_stage_bwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (a->bf16) {
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd<dtp::Stage<I, H, N, O, F, true>>(a, st);
+    DTP_STAGE_BF16_SHAPES(X)
+#undef X
+    return set_err(-2, "no bf16 instance of this mlp stage shape");
+  }
 #define X(I, H, N, O, F) \
   if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd<dtp::Stage<I, H, N, O, F>>(a, st);
   DTP_STAGE_SHAPES(X)

@@ -137,8 +137,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     if (NPT * tid + k < P) {
-      sm.wb[pfl[k]] = pw[k];
-      if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
+      const float wv = S::rnd(pw[k]);  // bf16 compute: the matmul operand is the bf16 weight
+      sm.wb[pfl[k]] = wv;
+      if (pb[k] >= 0) sm.wb[pb[k]] = wv;
     }
   }
   // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       di = r.valid ? di : 0;
       static_for<0, S::IN>([&](auto IC) {
         constexpr int i = decltype(IC)::value;
-        const float v = sm.data[di * S::IN + i];
+        const float v = S::rnd(sm.data[di * S::IN + i]);
         r.x[i] = r.valid ? v : 0.f;
       });
       static_for<0, S::OUT>([&](auto JC) {
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     if (r.valid) di = explicit_idx ? a.idx[(size_t)it_ * smp.batch + k] : sample_index(smp, bp_, keys_, k);
     static_for<0, S::IN>([&](auto IC) {
       constexpr int i = decltype(IC)::value;
-      r.x[i] = r.valid ? (cached ? sm.data[di * S::IN + i] : Xg[(size_t)di * S::IN + i]) : 0.f;
+      r.x[i] = r.valid ? S::rnd(cached ? sm.data[di * S::IN + i] : Xg[(size_t)di * S::IN + i]) : 0.f;
     });
     static_for<0, S::OUT>([&](auto JC) {
       constexpr int j = decltype(JC)::value;
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
           constexpr int j = decltype(JC)::value;
           const float d = h[L + 1][j] - smpl.y[j];
           lpart = valid ? fmaf(d, d, lpart) : lpart;
-          dz[j] = valid ? 2.f * d * inv : 0.f;
+          dz[j] = valid ? S::rnd(2.f * d * inv) : 0.f;
         });
       } else {
         const int cls = valid ? (int)smpl.y[0] : 0;
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
         lpart = valid ? lse - zc : 0.f;
         static_for<0, S::OUT>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
-          dz[j] = valid ? (__expf(h[L + 1][j] - mx) * rs - (j == cls ? 1.f : 0.f)) * inv : 0.f;
+          dz[j] = valid ? S::rnd((__expf(h[L + 1][j] - mx) * rs - (j == cls ? 1.f : 0.f)) * inv) : 0.f;
         });
       }
       if (c0 == 0) DTP_STAMP(2);
@@ -402,8 +403,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const bool own = NPT * tid + k < P;
-        *(own ? &sm.wb[pfl[k]] : &sm.sink[0]) = pw[k];
-        *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
+        const float wv = S::rnd(pw[k]);
+        *(own ? &sm.wb[pfl[k]] : &sm.sink[0]) = wv;
+        *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = wv;
       }
     }
     // the thread that holds the global loss logs it (xgmi_core.h: the loss granule's owner)
@@ -502,8 +504,20 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
          a.hp.slope >= 0.f && a.hp.slope <= 1.f;
 }
 
+// shapes with a bf16-compute instance (the toy model: MSE and CE heads)
+#define DTP_TRAIN_BF16_SHAPES(X) \
+  X(2, 10, 5, 1)                 \
+  X(2, 10, 5, 4)
+
 TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode) {
   const bool fast = fast_path_ok(a, in, out, mode);
+  if (a.bf16) {
+#define X(I, H, N, O) \
+  if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false, true>>(mode, fast);
+    DTP_TRAIN_BF16_SHAPES(X)
+#undef X
+    return nullptr;
+  }
 #define X(I, H, N, O) \
   if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false>>(mode, fast);
   DTP_TRAIN_SHAPES(X)
@@ -553,6 +567,14 @@ int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
 
 extern "C" {
 
+
+int dtp_mlp_train_bf16_supported(int in, int h, int nl, int out) {
+#define X(I, H, N, O) \
+  if (in == I && h == H && nl == N && out == O) return 1;
+  DTP_TRAIN_BF16_SHAPES(X)
+#undef X
+  return 0;
+}
 
 int dtp_mlp_workspace_floats(int in, int h, int nl, int out) {
 #define X(I, H, N, O) \

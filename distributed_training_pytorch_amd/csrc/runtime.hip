@@ -214,5 +214,7 @@ extern "C" int dtp_struct_sizes(int* out) {
   out[3] = (int)sizeof(DtpStageArgs);
   out[4] = (int)sizeof(DtpOptArgs);
   out[5] = (int)sizeof(DtpGemmArgs);
-  return 6;
+  out[6] = (int)sizeof(DtpSplitStageArgs);
+  out[7] = (int)sizeof(DtpSplitLaunch);
+  return 8;
 }

@@ -1,0 +1,363 @@
+// Persistent layer-split (inter-layer model parallel) training step for gfx950.
+//
+// Reference: MultiGPUModel (demo_one_model_multi_gpu.py:17-42) puts layers 0-1 on
+// dev0 and layers 2-4 on dev1, moves the [B,10] activation with .to(dev1) and lets
+// autograd copy the gradient back; DDP(device_ids=None) all-reduces per-device
+// buckets (:96-98); one Adam steps both stages (:107,128).  Host-driven, that is
+// ~10 launches, two peer copies and a bucketed all-reduce per iteration.
+//
+// Here every stage is ONE workgroup resident on its own GPU for n_steps
+// iterations (one lane per sample, batch <= 256), and the stages talk directly:
+//   * forward: the stage's output activation [B, OUT] is stored into the next
+//     stage's receive buffer as 16-byte granules {epoch, v0, v1, check} (one
+//     system-scope store each, peer-mapped over xGMI: posted writes, no copy
+//     engine, no host); the next stage's lanes poll their own granules;
+//   * backward: the input gradient [B, IN] goes back the same way;
+//   * the stage's weight gradient (MFMA dW tiles, mlp_core.h) is all-reduced over
+//     the data-parallel ranks INSIDE the step (xgmi_core.h; per-device buckets,
+//     overlapped for free: the last stage reduces while the first is still in its
+//     backward), then Adam / SGD updates the stage's weights in LDS and registers.
+// Epoch = global step + 1: a link buffer needs no parity -- stage s writes the
+// activation of step t+1 only after it received the gradient of step t, which the
+// next stage sends only after it consumed activation t (and symmetrically for the
+// gradient), so a granule is never overwritten while it is still unread.
+// Every spin is bounded (status word, then the step continues): a wedged
+// neighbour can never hang the GPU.
+#include "dtp_api.h"
+#include "mlp_core.h"
+#include "optim_core.h"
+#include "xgmi_core.h"
+
+namespace dtp {
+
+constexpr int kSplitCache = 8192;  // floats of dataset staged in LDS (first / last stage)
+
+// one lane's message: N floats as ceil(N/2) granules at granule index slot * G
+template <int N>
+DTP_DEV void link_send(void* buf, int slot, unsigned ep, const float (&v)[16], bool valid) {
+  constexpr int G = (N + 1) / 2;
+  if (!valid) return;
+  const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(buf);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t x0 = __float_as_uint(v[2 * g]), x1 = 2 * g + 1 < N ? __float_as_uint(v[2 * g + 1]) : 0u;
+    const u32x4 q = {ep, x0, x1, xgmi_check(ep, x0, x1)};
+    __builtin_amdgcn_raw_buffer_store_b128(q, rs, (slot * G + g) * 16, 0, kSysCoherent);
+  }
+}
+
+// poll this lane's granules of epoch ep in the local receive buffer (bounded)
+template <int N>
+DTP_DEV void link_recv(const void* buf, int slot, unsigned ep, float (&v)[16], bool valid, int* status,
+                       int timeout_us, bool& dead) {
+  constexpr int G = (N + 1) / 2;
+  static_assert(G <= 16, "message too wide");
+  const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(buf);
+  uint32_t pend = valid ? ((1u << G) - 1u) : 0u;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = 0.f;
+  const unsigned long long deadline =
+      __builtin_amdgcn_s_memrealtime() + (unsigned long long)(timeout_us > 0 ? timeout_us : 2000000) * 100ull;
+  while (pend && !dead) {
+    asm volatile("" ::: "memory");  // a poll is never merged with or hoisted above the previous one
+    u32x4 x[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      x[g] = u32x4{0u, 0u, 0u, 0u};
+      if ((pend >> g) & 1u) x[g] = __builtin_amdgcn_raw_buffer_load_b128(ms, (slot * G + g) * 16, 0, kSysCoherent);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (((pend >> g) & 1u) && x[g].x == ep && x[g].w == xgmi_check(ep, x[g].y, x[g].z)) {
+        v[2 * g] = __uint_as_float(x[g].y);
+        if (2 * g + 1 < N) v[2 * g + 1] = __uint_as_float(x[g].z);
+        pend &= ~(1u << g);
+      }
+    }
+    if (!pend) break;
+    if (__builtin_amdgcn_s_memrealtime() > deadline) {
+      dead = true;
+      if (status) {
+        atomicExch(&status[0], 1);
+        atomicExch(&status[1], (int)ep);
+      }
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <class S>
+struct SplitSmem {
+  float w[S::pad4(S::LP)];        // weights, row-major + transposed copies (mlp_core.h)
+  float stage[kBlock / kWave][2 * kStgArr];  // per-wave dW staging, reused for the cross-wave reduction
+  float data[kSplitCache];
+};
+
+constexpr int kSplitSmemBytes = 72 * 1024;  // the largest stage's SplitSmem
+
+// One pipeline stage, n_steps iterations.  FIRST: gathers the batch inputs from the
+// dataset; LAST: gathers the targets and computes the MSE loss; otherwise the
+// activation / gradient arrive over the links.  Runs as one workgroup of
+// split_multi_kernel (all the stages that share a GPU are one launch, so they are
+// co-resident by construction: no reliance on separate hardware queues).
+template <class S, bool FIRST, bool LAST>
+DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
+  constexpr int NL = S::NL, P = S::P, NPT = S::NPT;
+  static_assert(kBlock / kWave * NL * 256 <= kBlock / kWave * 2 * kStgArr, "reduction tiles fit the staging area");
+  static_assert(sizeof(SplitSmem<S>) <= kSplitSmemBytes, "stage LDS exceeds the shared block");
+  SplitSmem<S>& sm = *reinterpret_cast<SplitSmem<S>*>(smem);
+  const bool adam = a.optim == DTP_MODE_ADAM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const SamplerCfg smp = a.smp;
+  const float slope = a.hp.slope;
+  constexpr int XW = FIRST ? S::IN : 0;   // dataset columns this stage reads
+  constexpr int YW = LAST ? S::OUT : 0;
+
+  // ---- prologue: owned parameters + moments in registers, weights and dataset in LDS
+  float pw[NPT], mr[NPT], vr[NPT];
+  int tp[NPT], lp[NPT], lpt[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = NPT * tid + k;
+    const bool own = p < P;
+    pw[k] = own ? a.params[p] : 0.f;
+    mr[k] = own ? a.opt_m[p] : 0.f;
+    vr[k] = (own && adam) ? a.opt_v[p] : 0.f;
+    tp[k] = tile_pos<S>(own ? p : 0);
+    lp[k] = own ? lds_pos<S>(p) : -1;
+    lpt[k] = own ? lds_pos_t<S>(p) : -1;
+  }
+  for (int e = tid; e < S::pad4(S::LP); e += kBlock) sm.w[e] = 0.f;
+  const bool cached = a.cache_data && smp.n * (XW + YW) <= kSplitCache;
+  if (cached) {
+    if constexpr (FIRST)
+      for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
+    if constexpr (LAST)
+      for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * XW + e] = a.Y[e];
+  }
+  const int t0 = a.step[0];
+  __syncthreads();  // pads zeroed before the owners scatter
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    if (lp[k] >= 0) sm.w[lp[k]] = pw[k];
+    if (lpt[k] >= 0) sm.w[lpt[k]] = pw[k];
+  }
+  __syncthreads();
+
+  bool link_dead = __hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const XgmiCtx dp{a.dp_peers, a.status + 2, a.dp_world, a.dp_rank, 1, a.timeout_us};
+  const bool use_dp = a.dp_world > 1;
+  float* red = &sm.stage[0][0];
+
+  for (int it = 0; it < a.n_steps; ++it) {
+    const int t = t0 + it;
+    const unsigned ep = (unsigned)t + 1u;
+    const BatchPos bp = batch_pos(smp, t);
+    const int bsz = bp.size;
+    const bool valid = tid < bsz;
+    int di = 0;
+    if (FIRST || LAST) {
+      uint32_t keys[4];
+      epoch_keys(smp, bp.epoch, keys);
+      di = valid ? sample_index(smp, bp, keys, tid) : 0;
+    }
+    // ---- forward
+    float h[NL + 1][16];
+    if constexpr (FIRST) {
+      static_for<0, S::IN>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        h[0][i] = valid ? (cached ? sm.data[di * S::IN + i] : a.X[(size_t)di * S::IN + i]) : 0.f;
+      });
+    } else {
+      link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead);
+    }
+    mlp_forward<S>(sm.w, h, slope);
+
+    // ---- output gradient: from the next stage, or the MSE loss (last stage)
+    float dz[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dz[j] = 0.f;
+    const float inv = 1.f / (float)(bsz * S::OUT);
+    if constexpr (!LAST) {
+      link_send<S::OUT>(a.act_out, tid, ep, h[NL], valid);
+      float go[16];
+      link_recv<S::OUT>(a.grad_in, tid, ep, go, valid, a.status, a.timeout_us, link_dead);
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float d = S::FINAL_ACT ? go[j] * leaky_grad_from_out(h[NL][j], slope) : go[j];
+        dz[j] = valid ? d : 0.f;
+      });
+    } else {
+      float lpart = 0.f;
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float y = valid ? (cached ? sm.data[smp.n * XW + di * S::OUT + j] : a.Y[(size_t)di * S::OUT + j]) : 0.f;
+        const float d = h[NL][j] - y;
+        lpart = valid ? fmaf(d, d, lpart) : lpart;
+        dz[j] = valid ? 2.f * d * inv : 0.f;
+      });
+      dz[S::OUT] = lpart;  // loss row of the output tile (mlp_backward LOSS_ROW)
+    }
+
+    // ---- backward: input-gradient chain (VALU) + dW tiles (MFMA, K = samples)
+    f32x4 acc[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dx[16];
+    mlp_backward<S, !FIRST, LAST>(sm.w, h, dz, &sm.stage[wave][0], acc, slope, lane, dx);
+    if constexpr (!FIRST) link_send<S::IN>(a.grad_out, tid, ep, dx, valid);
+
+    // ---- reduce the per-wave tiles (staging area reused once every wave is done)
+    __syncthreads();
+    store_partial_tiles<S>(red, acc, wave, lane);
+    __syncthreads();
+    float g[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) g[k] = sum_partial_tiles<S>(red, tp[k], kBlock / kWave);
+    float loss = 0.f;
+    if constexpr (LAST) {
+      loss = sum_partial_tiles<S>(red, loss_tile_pos<S>(), kBlock / kWave) * inv;
+    }
+    // ---- data parallel: this stage's gradient (+ loss) summed over the ranks
+    float gloss = loss;
+    if (use_dp) gloss = xgmi_allreduce_slots<NPT>(dp, 0, P, g, loss, ep, tid);
+
+    // ---- optimizer (registers) + weight refresh (LDS)
+    const float gs = a.hp.grad_scale;
+    if (adam) {
+      const AdamScalars as = adam_scalars(a.hp, (long long)t + 1);
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        if (lp[k] >= 0) adam_update(pw[k], mr[k], vr[k], g[k] * gs, as);
+    } else {
+      const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        if (lp[k] >= 0) sgd_update(pw[k], mr[k], g[k] * gs, lr, mom, wd, t == 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if (lp[k] >= 0) sm.w[lp[k]] = pw[k];
+      if (lpt[k] >= 0) sm.w[lpt[k]] = pw[k];
+    }
+    if constexpr (LAST) {
+      const int owner = use_dp ? xgmi_loss_tid<NPT>(P, kBlock) : 0;
+      if (tid == owner && a.loss_log) a.loss_log[t % a.loss_log_cap] = use_dp ? gloss * gs : loss;
+    }
+    __syncthreads();  // new weights visible; reduction tiles consumed before the next staging writes
+  }
+
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = NPT * tid + k;
+    if (p < P) {
+      a.params[p] = pw[k];
+      a.opt_m[p] = mr[k];
+      if (adam) a.opt_v[p] = vr[k];
+    }
+  }
+  if (tid == 0) a.step[0] = t0 + a.n_steps;
+}
+
+// (IN, H, NL, OUT, FINAL_ACT, FIRST): the contiguous layer ranges of the toy model
+// as pipeline stages (first stages read the 2-feature input; stages that end inside
+// the network carry the LeakyReLU of their last layer and are not last); the shape
+// id of a stage is its position in this list
+#define DTP_SPLIT_SHAPES(X)   \
+  X(2, 10, 1, 10, true, 1)    \
+  X(2, 10, 2, 10, true, 1)    \
+  X(2, 10, 3, 10, true, 1)    \
+  X(2, 10, 4, 10, true, 1)    \
+  X(10, 10, 1, 10, true, 0)   \
+  X(10, 10, 2, 10, true, 0)   \
+  X(10, 10, 3, 10, true, 0)   \
+  X(10, 10, 1, 1, false, 0)   \
+  X(10, 10, 2, 1, false, 0)   \
+  X(10, 10, 3, 1, false, 0)   \
+  X(10, 10, 4, 1, false, 0)
+
+// every stage placed on one GPU, one workgroup each (blockIdx.x = local stage)
+__global__ __launch_bounds__(kBlock) void split_multi_kernel(DtpSplitLaunch) {
+  __shared__ __align__(16) unsigned char smem[kSplitSmemBytes];
+  const int b = blockIdx.x;
+  // this workgroup's stage arguments straight from the kernarg segment (uniform
+  // loads): indexing the by-value parameter with blockIdx would copy all of it to scratch
+  const DtpSplitLaunch* L = (const DtpSplitLaunch*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int shape = L->shape_id[b];
+  const DtpSplitStageArgs a = L->stage[b];
+  int id = 0;
+#define X(I, H, N, O, F, FI)                                                                \
+  if (shape == id) split_stage_body<Stage<I, H, N, O, F>, (bool)FI, !F>(a, smem); \
+  ++id;
+  DTP_SPLIT_SHAPES(X)
+#undef X
+}
+
+}  // namespace dtp
+
+extern "C" {
+
+long long dtp_split_link_bytes(int width, int batch) { return (long long)batch * ((width + 1) / 2) * 16ll; }
+
+// shape id of a stage (its position in DTP_SPLIT_SHAPES), -1 if not instantiated
+int dtp_split_shape_id(int in, int h, int nl, int out, int final_act, int first) {
+  int id = 0;
+#define X(I, H, N, O, F, FI)                                                                        \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F && (bool)first == (bool)FI) \
+    return id;                                                                                      \
+  ++id;
+  DTP_SPLIT_SHAPES(X)
+#undef X
+  return -1;
+}
+
+int dtp_split_stage_supported(int in, int h, int nl, int out, int final_act, int first) {
+  return dtp_split_shape_id(in, h, nl, out, final_act, first) >= 0;
+}
+
+static int validate_stage(const DtpSplitStageArgs* a, int first, int last) {
+  using dtp::set_err;
+  if (!a || !a->params || !a->opt_m || !a->step || !a->status) return set_err(-1, "split stage: missing buffers");
+  if (a->n_steps <= 0) return set_err(-1, "split stage: n_steps must be positive");
+  if (a->smp.batch <= 0 || a->smp.batch > dtp::kBlock || a->smp.mode == dtp::SAMPLER_EXPLICIT)
+    return set_err(-1, "split stage: batch must be 1..256 samples (one lane each) with a device sampler");
+  if (a->optim != DTP_MODE_ADAM && a->optim != DTP_MODE_SGD) return set_err(-1, "split stage: adam or sgd");
+  if (a->optim == DTP_MODE_ADAM && !a->opt_v) return set_err(-1, "split stage: Adam needs opt_v");
+  if (first && !a->X) return set_err(-1, "split stage: the first stage needs the inputs");
+  if (last && !a->Y) return set_err(-1, "split stage: the last stage needs the targets");
+  if (!first && (!a->act_in || !a->grad_out)) return set_err(-1, "split stage: missing links to the previous stage");
+  if (!last && (!a->act_out || !a->grad_in)) return set_err(-1, "split stage: missing links to the next stage");
+  if (last && a->loss_log && a->loss_log_cap <= 0) return set_err(-1, "split stage: loss_log_cap");
+  if (a->dp_world > 1 && (!a->dp_peers || a->dp_world > dtp::kXgmiMaxWorld || a->dp_rank < 0 ||
+                          a->dp_rank >= a->dp_world))
+    return set_err(-1, "split stage: data-parallel exchange serves 1..8 ranks with a peer table");
+  return 0;
+}
+
+// the stages of one GPU as ONE launch (co-resident workgroups)
+int dtp_split_launch(const DtpSplitLaunch* L, void* stream) {
+  using dtp::set_err;
+  if (!L || L->n < 1 || L->n > DTP_SPLIT_MAX_LOCAL) return set_err(-1, "split launch: 1..8 stages per GPU");
+  static const int first_of[] = {
+#define X(I, H, N, O, F, FI) FI,
+      DTP_SPLIT_SHAPES(X)
+#undef X
+  };
+  static const int last_of[] = {
+#define X(I, H, N, O, F, FI) !F,
+      DTP_SPLIT_SHAPES(X)
+#undef X
+  };
+  constexpr int nshapes = sizeof(first_of) / sizeof(first_of[0]);
+  for (int i = 0; i < L->n; ++i) {
+    const int id = L->shape_id[i];
+    if (id < 0 || id >= nshapes) return set_err(-2, "split launch: stage shape not instantiated");
+    if (int rc = validate_stage(&L->stage[i], first_of[id], last_of[id])) return rc;
+    if (L->stage[i].n_steps != L->stage[0].n_steps) return set_err(-1, "split launch: stages disagree on n_steps");
+  }
+  hipLaunchKernelGGL(dtp::split_multi_kernel, dim3(L->n), dim3(dtp::kBlock), 0, (hipStream_t)stream, *L);
+  return dtp::check_launch("split_multi_kernel");
+}
+
+}  // extern "C"

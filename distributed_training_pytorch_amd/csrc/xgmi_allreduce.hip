@@ -14,6 +14,13 @@
 // [parity 2][src rank W][cap] granules.  The epoch increases by one per call on
 // every rank (calls are stream-ordered), so a fast rank is at most one call
 // ahead of a slow one and never overwrites a parity still being read.
+//
+// The epoch lives in DEVICE memory, one counter per workgroup (a workgroup always
+// owns the same granule range, so its counter counts exactly the calls that used
+// those granules, identically on every rank): the kernel reads and advances it
+// itself, so a hipGraph replay of a captured call is a new exchange -- no host
+// state changes per call, and the module engine / Trainer capture their whole
+// step, xGMI buckets included.
 #include "dtp_api.h"
 #include "dtp_common.h"
 
@@ -25,8 +32,12 @@ constexpr int kArMaxWorld = 8;
 
 __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(float* __restrict__ data, int n, int cap,
                                                                       unsigned long long* const* __restrict__ peers,
-                                                                      int world, int rank, unsigned epoch,
+                                                                      int world, int rank, unsigned* epochs,
                                                                       float scale, int* status, int timeout_us) {
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[blockIdx.x] + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
   const int base = (blockIdx.x * kArThreads + threadIdx.x) * kArPerThread;
   const size_t par = epoch & 1u;
   float v[kArPerThread];
@@ -92,19 +103,29 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(float* __res
     for (int r = 0; r < kArMaxWorld; ++r) s += got[r][k];  // rank order; absent ranks add +0
     data[base + k] = s * scale;
   }
+  // the next call of this workgroup (a later kernel on the stream) sees the new epoch
+  if (threadIdx.x == 0) epochs[blockIdx.x] = epoch;
 }
 
 }  // namespace dtp
 
+// epochs: device counters, one per workgroup of a capacity-sized call
+// (dtp_xgmi_allreduce_epoch_slots(cap)), zeroed before the first call on every rank
+extern "C" int dtp_xgmi_allreduce_epoch_slots(int cap) {
+  const int per_block = dtp::kArThreads * dtp::kArPerThread;
+  return (cap + per_block - 1) / per_block;
+}
+
 extern "C" int dtp_xgmi_allreduce(float* data, int n, int cap, void* const* peers, int world, int rank,
-                                  unsigned epoch, float scale, int* status, int timeout_us, void* stream) {
-  if (!data || !peers || n < 0 || n > cap) return dtp::set_err(-1, "dtp_xgmi_allreduce: bad buffer or size > capacity");
+                                  unsigned* epochs, float scale, int* status, int timeout_us, void* stream) {
+  if (!data || !peers || !epochs || n < 0 || n > cap)
+    return dtp::set_err(-1, "dtp_xgmi_allreduce: bad buffer, no epoch counters, or size > capacity");
   if (world < 1 || world > dtp::kArMaxWorld || rank < 0 || rank >= world)
     return dtp::set_err(-1, "dtp_xgmi_allreduce: world must be 1..8");
   if (n == 0) return 0;
   const int per_block = dtp::kArThreads * dtp::kArPerThread;
   hipLaunchKernelGGL(dtp::xgmi_allreduce_kernel, dim3((n + per_block - 1) / per_block), dim3(dtp::kArThreads), 0,
-                     (hipStream_t)stream, data, n, cap, (unsigned long long* const*)peers, world, rank, epoch, scale,
+                     (hipStream_t)stream, data, n, cap, (unsigned long long* const*)peers, world, rank, epochs, scale,
                      status, timeout_us);
   return dtp::check_launch("xgmi_allreduce_kernel");
 }

@@ -87,11 +87,21 @@ DTP_DEV __amdgpu_buffer_rsrc_t xgmi_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
+// Who takes part in one exchange: every rank's receive buffer (peer-mapped), this
+// rank's place, the sticky status word and the spin bound.  The fused train step
+// builds it from its DtpTrainArgs; the layer-split stage kernels (split_train.hip)
+// use one per pipeline stage (the stage's gradient reduced over the ranks).
+struct XgmiCtx {
+  float* const* peers;
+  int* status;
+  int world, rank, n_models, timeout_us;
+};
+
 template <int NPT, int NTHREADS = kBlock>
-DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
-                                   unsigned epoch, int tid) {
+DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g)[NPT], float loss, unsigned epoch,
+                                   int tid) {
   constexpr int GPT = xgmi_gpt<NPT>();
-  const int W = a.smp.world, R = a.smp.rank;
+  const int W = a.world, R = a.rank;
   const int slot = xgmi_slot16(P, NPT);
   const int nthr = xgmi_nthr(P, NPT);
   const int ltid = xgmi_loss_tid<NPT>(P, NTHREADS);
@@ -228,6 +238,13 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
 #pragma unroll
   for (int r = 0; r < kXgmiMaxWorld; ++r) lacc += val[r][GPT][0];
   return lacc;
+}
+
+template <int NPT, int NTHREADS = kBlock>
+DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
+                                   unsigned epoch, int tid) {
+  const XgmiCtx c{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
+  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid);
 }
 
 }  // namespace dtp

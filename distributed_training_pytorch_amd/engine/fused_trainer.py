@@ -46,6 +46,7 @@ class EngineConfig:
     xgmi_timeout_us: int = 2_000_000  # per exchange; sticky once hit (never multiplies over steps)
     xgmi_selftest: bool = True        # validate the xGMI exchange against a host all-reduce, else fall back
     rccl_graph: bool = True      # capture grad->all_reduce->optimizer into a hipGraph
+    precision: str = "fp32"      # fp32 | bf16 (bf16 matmul operands, fp32 accumulation / master weights / Adam)
 
 
 class FusedTrainer:
@@ -57,6 +58,8 @@ class FusedTrainer:
         self.n_models = n_models
         self.optim = optim or OptimConfig()
         self.cfg = cfg or EngineConfig()
+        if self.cfg.precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision {self.cfg.precision!r}: fp32 or bf16")
         self.geom = geom
         self.group = group
         self.device = X.device
@@ -97,6 +100,8 @@ class FusedTrainer:
             if not spec.native_supported():
                 raise NotImplementedError(f"no fused kernel for {spec}")
             lib = nat.require(self.device)
+            if self.cfg.precision == "bf16" and not lib.dtp_mlp_train_bf16_supported(*spec.key[:4]):
+                raise NotImplementedError(f"no bf16 fused train kernel for {spec}")
             ws = lib.dtp_mlp_workspace_floats(spec.in_features, spec.hidden, spec.n_layers, spec.out_features)
             if ws <= 0:
                 raise NotImplementedError(f"no fused train kernel for {spec}")
@@ -245,7 +250,7 @@ class FusedTrainer:
             nat.ptr(xg.epoch) if xg else None, nat.ptr(getattr(self, "wsp", None)),
             self.loss_log.shape[0], self.n_models, n_steps,
             nat.LOSS_CE if self.cfg.loss == "ce" else nat.LOSS_MSE,
-            int(self.cfg.cache_data), self.cfg.xgmi_timeout_us, smp,
+            int(self.cfg.cache_data), self.cfg.xgmi_timeout_us, int(self.cfg.precision == "bf16"), 0, smp,
             # xGMI modes sum the W gradients in-kernel -> DDP averaging 1/W there;
             # MODE_GRAD writes local means (the flat optimizer applies 1/W)
             self._hyper(1.0 / self.world if mode in (nat.MODE_XGMI_ADAM, nat.MODE_XGMI_SGD) else 1.0))

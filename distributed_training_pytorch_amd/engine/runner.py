@@ -88,11 +88,15 @@ def _compute_dtype(config) -> torch.dtype:
 
 
 def _fused_supported(config) -> bool:
+    from .. import _native as nat
     from ..ops.mlp import MlpSpec
 
-    if _compute_dtype(config) != torch.float32:
-        return False
     spec = MlpSpec(2, config.hidden, config.depth + 2, 4 if config.loss == "ce" else 1)
+    if _compute_dtype(config) == torch.bfloat16:
+        try:
+            return bool(nat.load().dtp_mlp_train_bf16_supported(*spec.key[:4]))
+        except nat.NativeUnavailable:
+            return False
     return spec.native_supported()
 
 
@@ -151,7 +155,7 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
     init = [ToyModel(hidden=config.hidden, depth=config.depth, out_features=out_f).flat_params.detach().clone()
             for _ in range(2)]
     ecfg = EngineConfig(comm=config.comm, launch=config.launch, steps_per_launch=config.steps_per_launch,
-                        sampler=config.sampler, loss=config.loss)
+                        sampler=config.sampler, loss=config.loss, precision=config.precision)
     tr = FusedTrainer(spec, 2, X, Y, geom, _optim(config), ecfg, init_params=init)
     start = 0
     if config.resume and config.checkpoint_dir:
@@ -315,9 +319,9 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
         ring.put_device(lx, ly)
 
     # hipGraph replay of the whole iteration (engine/graph_step.py) where it can be
-    # captured: one rank, or RCCL buckets (the xGMI bucket path and gloo are host-driven)
-    graphable = device.type == "cuda" and config.launch != "eager" and not trace_enabled() and (
-        world == 1 or (dist.get_backend() == "nccl" and ddp.comm == "rccl"))
+    # captured: one rank, xGMI buckets (device-side exchange epochs) or RCCL buckets;
+    # not gloo-staged buckets (host-driven)
+    graphable = device.type == "cuda" and config.launch != "eager" and not trace_enabled() and ddp.graph_safe()
     stepper = CapturedStep(step_body, device, enabled=graphable, on_abort=ddp.reset_hooks)
     for it in range(start, config.iters):
         faults.check(it)

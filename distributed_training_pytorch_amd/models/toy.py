@@ -8,9 +8,12 @@ built for the fused HIP path.
   use.  The packing survives ``.to()/.cuda()`` (re-flattened in ``_apply``).
 * On a CUDA input the forward is ONE fused kernel and the backward ONE fused
   kernel (``ops.mlp.FusedMLPFunction``); on CPU it is plain PyTorch.
+* bf16 compute (``compute_dtype=torch.bfloat16`` or an enclosing
+  ``torch.autocast(dtype=bfloat16)``): the bf16 instances of the same fused kernels
+  (bf16 matmul operands, fp32 accumulation, fp32 master weights and gradients).
 * Widths the fused kernel does not cover (hidden > 15) run every Linear on the
   MFMA GEMM with fused bias/LeakyReLU epilogues (``ops.gemm.mlp``), in fp32 or
-  with bf16 compute (``compute_dtype``; fp32 master weights and gradients).
+  with bf16 compute.
 """
 from __future__ import annotations
 
@@ -74,7 +77,7 @@ class ToyModel(nn.Module):
                 cd = torch.get_autocast_dtype("cuda")
             if cd == torch.float32 and self.uses_fused_kernel():
                 return fused_mlp(x.float(), self.spec, list(self.layers.parameters()))
-            if cd == torch.bfloat16 and self.spec.native_supported():
+            if cd == torch.bfloat16 and self.spec.native_supported(bf16=True):
                 # fused stage kernels in bf16 compute: bf16 weights/activations, fp32
                 # accumulation, fp32 master weights and gradients
                 return fused_mlp(x.float(), self.spec, list(self.layers.parameters()), bf16=True)

@@ -68,12 +68,12 @@ class MlpSpec:
     def key(self) -> tuple[int, int, int, int, int]:
         return (self.in_features, self.hidden, self.n_layers, self.out_features, int(self.final_act))
 
-    def native_supported(self) -> bool:
+    def native_supported(self, bf16: bool = False) -> bool:
         try:
             lib = nat.load()
         except nat.NativeUnavailable:
             return False
-        return bool(lib.dtp_mlp_supported(*self.key))
+        return bool(lib.dtp_mlp_supported_bf16(*self.key) if bf16 else lib.dtp_mlp_supported(*self.key))
 
 
 TOY_SPEC = MlpSpec()
@@ -114,10 +114,12 @@ def _check_f32_cuda(name: str, t: torch.Tensor, device: torch.device, numel: int
 
 
 def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool = True,
-                  peer_device: torch.device | None = None):
+                  peer_device: torch.device | None = None, force_peer: bool = False, bf16: bool = False):
     """Native forward of one MLP stage. Returns (out [B,OUT], saved [B,(NL-1)*H] or None)
     or, with peer_device, (out, saved, out_peer) where out_peer lives on peer_device and is
-    written by the same kernel over xGMI (peer access must be enabled)."""
+    written by the same kernel over xGMI (peer access must be enabled).  ``force_peer``
+    makes the epilogue's second store target a distinct buffer even when peer_device is
+    x's own device (tests of the hand-off path on a one-GPU box)."""
     lib = nat.require(x.device)
     if x.dim() != 2 or x.shape[1] != spec.in_features:
         raise ValueError(f"input must be [B, {spec.in_features}], got {tuple(x.shape)}")
@@ -129,10 +131,10 @@ def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool
     saved = torch.empty(B, (spec.n_layers - 1) * spec.hidden, device=dev, dtype=torch.float32) \
         if (save and spec.n_layers > 1) else None
     out_peer = None
-    if peer_device is not None and torch.device(peer_device) != dev:
+    if peer_device is not None and (torch.device(peer_device) != dev or force_peer):
         out_peer = torch.empty(B, spec.out_features, device=peer_device, dtype=torch.float32)
     a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), None, None, None, nat.ptr(out_peer),
-                      B, spec.slope)
+                      B, spec.slope, 0, int(bf16))
     nat.check(lib.dtp_mlp_stage_fwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_fwd")
     if peer_device is not None:
         return out, saved, (out_peer if out_peer is not None else out)
@@ -140,7 +142,7 @@ def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool
 
 
 def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: bool = True,
-                   grad_params: torch.Tensor | None = None):
+                   grad_params: torch.Tensor | None = None, bf16: bool = False):
     """Native backward of one stage. Returns (grad_in or None, grad_params [P]).
 
     With ``grad_params`` (a contiguous fp32 [P] span, e.g. the parameters' persistent
@@ -164,7 +166,7 @@ def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: b
         gp = torch.zeros(spec.P, device=dev, dtype=torch.float32) if nblk > 1 else \
             torch.empty(spec.P, device=dev, dtype=torch.float32)
     a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), nat.ptr(grad_out),
-                      nat.ptr(grad_in), nat.ptr(gp), None, B, spec.slope, int(acc))
+                      nat.ptr(grad_in), nat.ptr(gp), None, B, spec.slope, int(acc), int(bf16))
     nat.check(lib.dtp_mlp_stage_bwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_bwd")
     return grad_in, gp
 
@@ -191,14 +193,15 @@ class FusedMLPFunction(torch.autograd.Function):
     reduction) each in ONE kernel, instead of ~9 GEMM + ~10 elementwise launches."""
 
     @staticmethod
-    def forward(ctx, x, spec: MlpSpec, *params):
+    def forward(ctx, x, spec: MlpSpec, bf16: bool, *params):
         flat = _flat_view_of(list(params))
         if flat is None:
             flat = torch.cat([p.detach().reshape(-1) for p in params])
         flat = flat.detach()
         x = x.contiguous()
-        out, saved = stage_forward(x, flat, spec, save=True)
+        out, saved = stage_forward(x, flat, spec, save=True, bf16=bf16)
         ctx.spec = spec
+        ctx.bf16 = bf16
         ctx.shapes = [p.shape for p in params]
         ctx.params = params
         ctx.save_for_backward(x, flat, out, saved if saved is not None else torch.empty(0, device=x.device))
@@ -213,14 +216,14 @@ class FusedMLPFunction(torch.autograd.Function):
         # (ModelBank / FlatDDP, ops.gemm.mark_fused_grad): the kernel adds into it, so
         # autograd runs no AccumulateGrad add kernel per parameter tensor
         target = None
-        if all(ctx.needs_input_grad[2:]) and all(_fused_grad_target(p) is not None for p in params):
+        if all(ctx.needs_input_grad[3:]) and all(_fused_grad_target(p) is not None for p in params):
             target = _flat_view_of([p.grad for p in params])
-        gin, gp = stage_backward(x, flat, spec, out, saved if saved.numel() else None, grad_out,
-                                 need_grad_in=ctx.needs_input_grad[0], grad_params=target)
+        gin, gp = stage_backward(x, flat, spec, out, saved if saved.numel() else None, grad_out.float(),
+                                 need_grad_in=ctx.needs_input_grad[0], grad_params=target, bf16=ctx.bf16)
         if target is not None:
             for p in params:
                 _grad_ready(p)
-            return (gin, None, *([None] * len(params)))
+            return (gin, None, None, *([None] * len(params)))
         grads, o = [], 0
         for shp in ctx.shapes:
             n = 1
@@ -228,14 +231,44 @@ class FusedMLPFunction(torch.autograd.Function):
                 n *= s
             grads.append(gp[o:o + n].view(shp))
             o += n
-        return (gin, None, *grads)
+        return (gin, None, None, *grads)
 
 
-def fused_mlp(x: torch.Tensor, spec: MlpSpec, params: list[torch.Tensor]) -> torch.Tensor:
+def fused_mlp(x: torch.Tensor, spec: MlpSpec, params: list[torch.Tensor], bf16: bool = False) -> torch.Tensor:
+    """The whole MLP as one fused forward and one fused backward kernel.  ``bf16``:
+    bf16 compute (bf16 weights / activations / gradients as matmul operands, fp32
+    accumulation, fp32 weight gradients -- torch.autocast's recipe)."""
     if x.is_cuda and nat.native_enabled():
-        if not spec.native_supported():
-            nat.require(x.device)  # raises if the library is missing
-            raise NotImplementedError(f"no fused kernel instantiated for {spec}")
-        return FusedMLPFunction.apply(x, spec, *params)
+        lib = nat.require(x.device)  # raises if the library is missing
+        ok = lib.dtp_mlp_supported_bf16(*spec.key) if bf16 else spec.native_supported()
+        if not ok:
+            raise NotImplementedError(f"no fused {'bf16 ' if bf16 else ''}kernel instantiated for {spec}")
+        return FusedMLPFunction.apply(x, spec, bool(bf16), *params)
     flat = torch.cat([p.reshape(-1) for p in params])
     return mlp_forward_ref(flat, spec, x)
+
+
+def bf16_round(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def mlp_forward_ref_bf16(flat: torch.Tensor, spec: MlpSpec, x: torch.Tensor) -> torch.Tensor:
+    """PyTorch reference of the bf16-compute kernels (fp32 tensors holding bf16 values:
+    bf16 operands, fp32 accumulation, bf16 rounding of every matmul output and
+    activation) -- differentiable, its backward rounds the gradients the same way."""
+    class _R(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, t):
+            return bf16_round(t)
+
+        @staticmethod
+        def backward(ctx, g):
+            return bf16_round(g)
+
+    ps = unflatten(flat, spec)
+    h = _R.apply(x)
+    for l in range(spec.n_layers):
+        h = _R.apply(F.linear(h, _R.apply(ps[2 * l]), _R.apply(ps[2 * l + 1])))
+        if spec.act(l):
+            h = _R.apply(F.leaky_relu(h, spec.slope))
+    return h

@@ -207,6 +207,18 @@ class FlatDDP(nn.Module):
         self._works = []
         self._callback_queued = False
 
+    def graph_safe(self) -> bool:
+        """Can a backward through this wrapper be captured into a hipGraph?  Yes with
+        one rank, when every bucket goes through the in-kernel xGMI all-reduce (its
+        exchange epochs are device counters, so each replay is a fresh exchange), or
+        when the remaining buckets ride RCCL (capturable collectives); not when a
+        bucket is staged through gloo on the host."""
+        if self.world == 1:
+            return True
+        if all(b in self._xgmi_buckets for b in range(len(self._buckets))):
+            return True
+        return dist.get_backend(self.group) == "nccl"
+
     def check_comm(self):
         """Raise if an xGMI all-reduce timed out (one host sync; call at log points)."""
         if self._xgmi is not None:

@@ -28,7 +28,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import _native as nat
-from ..ops.gemm import _fused_grad_target, _grad_ready, mark_fused_grad
+from ..ops.gemm import _fused_grad_target, _grad_ready, add_grad_ready_hook, mark_fused_grad
 from ..ops.mlp import MlpSpec, mlp_forward_ref, stage_backward, stage_forward
 from . import comm_util
 
@@ -68,10 +68,10 @@ class _PeerStageFn(torch.autograd.Function):
     grad_out from `dst` through the same peer mapping (no staging copies)."""
 
     @staticmethod
-    def forward(ctx, x, flat, spec: MlpSpec, dst: torch.device):
+    def forward(ctx, x, flat, spec: MlpSpec, dst: torch.device, force_peer: bool = False):
         src = x.device
         with torch.cuda.device(src):
-            out, saved, out_dst = stage_forward(x, flat, spec, save=True, peer_device=dst)
+            out, saved, out_dst = stage_forward(x, flat, spec, save=True, peer_device=dst, force_peer=force_peer)
             if dst != src:  # the consumer's stream waits for the producing kernel
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(src))
@@ -106,14 +106,17 @@ class _PeerStageFn(torch.autograd.Function):
             # the kernel already added into .grad: autograd has nothing to accumulate,
             # and the grad-ready hooks (per-stage DDP buckets) fire here instead
             _grad_ready(ctx.param)
-            return gin, None, None, None
-        return gin, gp, None, None
+            return gin, None, None, None, None
+        return gin, gp, None, None, None
 
 
 class LayerSplitMLP(nn.Module):
     def __init__(self, spec: MlpSpec, devices: list[torch.device], boundaries: list[tuple[int, int]] | None = None,
-                 microbatches: int = 1, init_flat: torch.Tensor | None = None):
+                 microbatches: int = 1, init_flat: torch.Tensor | None = None, force_peer_buffers: bool = False):
         super().__init__()
+        # tests: hand activations over through the epilogue's second (peer) store even
+        # between stages on the same GPU, as they are between distinct GPUs
+        self.force_peer_buffers = force_peer_buffers
         self.spec = spec
         self.devices = [torch.device(d) for d in devices]
         self.boundaries = boundaries or default_boundaries(spec.n_layers, len(self.devices))
@@ -144,7 +147,7 @@ class LayerSplitMLP(nn.Module):
 
     def _stage(self, s: int, x: torch.Tensor, dst: torch.device) -> torch.Tensor:
         if self.native:
-            return _PeerStageFn.apply(x, self.params[s], self.stage_specs[s], dst)
+            return _PeerStageFn.apply(x, self.params[s], self.stage_specs[s], dst, self.force_peer_buffers)
         return mlp_forward_ref(self.params[s], self.stage_specs[s], x).to(dst)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -177,38 +180,339 @@ class LayerSplitMLP(nn.Module):
 
 
 class LayerSplitDDP:
-    """Data parallel on top of a layer-split model: every stage's gradient is packed
-    into one flat buffer on the first stage's device and all-reduced once."""
+    """Data parallel on top of a layer-split model, the way ``DDP(model,
+    device_ids=None)`` treats a multi-device module (``demo_one_model_multi_gpu.py:
+    96-98``): one gradient bucket PER DEVICE (per stage), each all-reduced as soon as
+    that stage's backward has produced it -- from the stage parameter's grad-ready
+    hook, on a side stream of the stage's own device -- so the last stage's bucket is
+    on the wire while the earlier stages are still in their backward.
 
-    def __init__(self, model: LayerSplitMLP, group=None):
+    Per bucket: the in-kernel xGMI one-shot all-reduce (``comm`` auto/xgmi, <= 8 ranks,
+    buffers on the stage's device), RCCL (async work on the stage's device), or gloo
+    (host-staged, CPU tests).  ``finish()`` (or the autograd end-of-backward callback)
+    joins the streams; the averaging (1/W) is folded into the reduction."""
+
+    def __init__(self, model: LayerSplitMLP, group=None, comm: str = "auto"):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        dev = model.devices[0]
-        self.sizes = [p.numel() for p in model.params]
-        self.buf = torch.zeros(sum(self.sizes), device=dev)
-        if self.world > 1:  # construction broadcast of rank 0's parameters
-            o = 0
-            for p, n in zip(model.params, self.sizes):
-                self.buf[o:o + n].copy_(p.detach().reshape(-1))
-                o += n
-            comm_util.broadcast_(self.buf, 0, group)
-            o = 0
+        self.params = list(model.params)
+        # construction broadcast of rank 0's parameters (per stage, on the stage's device)
+        if self.world > 1:
             with torch.no_grad():
-                for p, n in zip(model.params, self.sizes):
-                    p.copy_(self.buf[o:o + n].view_as(p))
-                    o += n
+                for p in self.params:
+                    comm_util.broadcast_(p.data, 0, group)
+        self._xgmi: dict = {}
+        self._side: dict = {}
+        self.comm = "none" if self.world == 1 else ("gloo" if dist.get_backend(group) == "gloo" else "rccl")
+        if self.world > 1 and comm in ("auto", "xgmi") and all(p.is_cuda for p in self.params):
+            self._setup_xgmi(strict=comm == "xgmi")
+        for p in self.params:
+            p.register_post_accumulate_grad_hook(self._hook)
+            add_grad_ready_hook(p, self._hook)
+        self._pending: list = []
+        self._queued = False
+        self._done: set = set()
 
-    def allreduce_grads(self):
+    def _setup_xgmi(self, strict: bool):
+        from .xgmi import XgmiAllReduce
+
+        ok, ars, why = True, {}, ""
+        try:
+            for i, p in enumerate(self.params):
+                with torch.cuda.device(p.device):
+                    ars[i] = XgmiAllReduce(p.numel(), p.device, self.group)
+        except Exception as e:  # noqa: BLE001 - any mapping failure -> process-group buckets
+            ok, why = False, str(e)
+        flag = torch.tensor([1.0 if ok else 0.0])
+        comm_util.all_reduce_(flag, self.group, op=dist.ReduceOp.MIN)
+        if flag.item() == 1.0:
+            self._xgmi = ars
+            self._side = {i: torch.cuda.Stream(p.device) for i, p in enumerate(self.params)}
+            self.comm = "xgmi"
+            return
+        for ar in ars.values():
+            ar.close()
+        if strict:
+            raise RuntimeError(f"LayerSplitDDP comm='xgmi' unavailable: {why or 'a peer failed'}")
+
+    def _hook(self, p):
+        if not self._queued:
+            torch.autograd.Variable._execution_engine.queue_callback(self.finish)
+            self._queued = True
+        i = next(k for k, q in enumerate(self.params) if q is p)
+        if i in self._done:
+            return
+        self._done.add(i)
+        self._reduce(i)
+
+    def _reduce(self, i: int):
         if self.world == 1:
             return
+        p = self.params[i]
+        g = p.grad.view(-1)
+        if i in self._xgmi:
+            side = self._side[i]
+            side.wait_stream(torch.cuda.current_stream(p.device))
+            with torch.cuda.stream(side):
+                self._xgmi[i].all_reduce_(g, scale=1.0 / self.world)
+            self._pending.append(("xgmi", i))
+        elif dist.get_backend(self.group) == "nccl":
+            with torch.cuda.device(p.device):
+                w = dist.all_reduce(g, group=self.group, async_op=True)
+            self._pending.append((w, i))
+        else:
+            comm_util.all_reduce_(g, self.group)
+            g.mul_(1.0 / self.world)
+            self._pending.append((None, i))
+
+    def finish(self):
+        """Join every bucket's reduction (idempotent; also the end-of-backward callback)."""
+        for i in range(len(self.params)):  # stages that produced no gradient this backward
+            if i not in self._done:
+                self._done.add(i)
+                self._reduce(i)
+        for w, i in self._pending:
+            p = self.params[i]
+            if w == "xgmi":
+                torch.cuda.current_stream(p.device).wait_stream(self._side[i])
+            elif w is not None:
+                w.wait()
+                p.grad.mul_(1.0 / self.world)
+        self._pending = []
+        self._done = set()
+        self._queued = False
+
+    # the reference calls optimizer.step() right after backward: kept as an explicit
+    # join for callers that drive the buckets themselves
+    allreduce_grads = finish
+
+    def check_comm(self):
+        for ar in self._xgmi.values():
+            ar.check()
+
+    def close(self):
+        for ar in self._xgmi.values():
+            ar.close()
+        self._xgmi = {}
+
+
+class FusedLayerSplit:
+    """The layer-split model as persistent stage kernels (``csrc/split_train.hip``):
+    stage s is ONE workgroup resident on ``devices[s]`` for every iteration of a
+    ``train(k)`` call, sending its activation to stage s+1 and its input gradient to
+    stage s-1 as epoch-tagged granules stored straight into the neighbour GPU's
+    receive buffer (peer-mapped over xGMI), reducing its weight gradient over the
+    data-parallel ranks in-kernel (per-device buckets, overlapped with the other
+    stages' backward), with Adam / SGD fused.  The host issues one launch per stage
+    per ``train(k)``; losses stay in a device ring on the last stage's GPU.
+
+    Same semantics as the reference loop (``demo_one_model_multi_gpu.py:118-138``):
+    forward through every stage, MSE on the last, backward, averaged gradients,
+    one optimizer step per iteration; the sampler is the device DistributedSampler
+    (``data/sampler.py``)."""
+
+    def __init__(self, spec: MlpSpec, devices: list[torch.device], X: torch.Tensor, Y: torch.Tensor, geom,
+                 optim, init_flat: torch.Tensor, boundaries: list[tuple[int, int]] | None = None, group=None,
+                 timeout_us: int = 2_000_000, log_cap: int = 1 << 16):
+        import ctypes
+
+        from ..ops.optim import OptimConfig
+
+        self.spec = spec
+        self.devices = [torch.device(d) for d in devices]
+        K = len(self.devices)
+        self.bounds = boundaries or default_boundaries(spec.n_layers, K)
+        self.stage_specs = [spec.substage(a, b) for a, b in self.bounds]
+        self.optim = optim or OptimConfig()
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if geom.world != self.world or geom.rank != self.rank:
+            raise ValueError("sampler geometry does not match the process group")
+        if geom.batch > 256:
+            raise ValueError("the persistent split step runs one lane per sample: per-rank batch <= 256")
+        self.geom = geom
+        self.lib = lib = nat.require(self.devices[0])
+        for s, ss in enumerate(self.stage_specs):
+            if not lib.dtp_split_stage_supported(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
+                                                 int(ss.final_act), int(s == 0)):
+                raise NotImplementedError(f"no persistent split-stage kernel for stage {s}: {ss}")
+        init = init_flat.detach().float().cpu().clone()
+        if self.world > 1:  # DDP construction semantics: rank 0's weights everywhere
+            comm_util.broadcast_(init, 0, group)
+        for d0, d1 in zip(self.devices[:-1], self.devices[1:]):
+            _enable_peer(d0, d1)
+            _enable_peer(d1, d0)
+        self.params, self.m, self.v, self.step, self.status = [], [], [], [], []
+        for (a, b), dev in zip(self.bounds, self.devices):
+            lo, hi = spec.param_range(a, b)
+            self.params.append(init[lo:hi].to(dev))
+            self.m.append(torch.zeros(hi - lo, device=dev))
+            self.v.append(torch.zeros(hi - lo, device=dev))
+            self.step.append(torch.zeros(1, dtype=torch.int32, device=dev))
+            self.status.append(torch.zeros(16, dtype=torch.int32, device=dev))
+        self.loss_log = torch.zeros(log_cap, device=self.devices[-1])
+        self.X = X.to(self.devices[0]).contiguous().float()
+        self.Y = Y.to(self.devices[-1]).contiguous().float()
+        # link buffers: act into stage s+1 (on its device), grad into stage s (on its device)
+        self._owned: list[tuple[int, int]] = []  # (device index, pointer)
+        self.act_buf, self.grad_buf = [None] * K, [None] * K
+        for s in range(K - 1):
+            width = self.stage_specs[s].out_features
+            nbytes = int(lib.dtp_split_link_bytes(width, geom.batch))
+            self.act_buf[s + 1] = self._alloc(self.devices[s + 1], nbytes)
+            self.grad_buf[s] = self._alloc(self.devices[s], nbytes)
+        # per-stage data-parallel exchange (the stage's gradient over the ranks)
+        self._dp = [None] * K
+        if self.world > 1:
+            from .xgmi import PeerBuffers
+
+            for s, (ss, dev) in enumerate(zip(self.stage_specs, self.devices)):
+                with torch.cuda.device(dev):
+                    self._dp[s] = PeerBuffers(int(lib.dtp_xgmi_fused_buffer_bytes(ss.P, 1, self.world)), dev, group)
+        # the stages that share a GPU run as ONE launch (one workgroup each: co-resident
+        # by construction); one stream per GPU
+        self.groups: dict[torch.device, list[int]] = {}
+        for s, dev in enumerate(self.devices):
+            self.groups.setdefault(dev, []).append(s)
+        if any(len(v) > nat.SPLIT_MAX_LOCAL for v in self.groups.values()):
+            raise ValueError(f"at most {nat.SPLIT_MAX_LOCAL} stages per GPU")
+        self.streams = {dev: torch.cuda.Stream(device=dev) for dev in self.groups}
+        self.t = 0
+        self._launch = {}
+        for dev, stages in self.groups.items():
+            L = nat.SplitLaunch()
+            L.n = len(stages)
+            for j, s in enumerate(stages):
+                ss = self.stage_specs[s]
+                a = L.stage[j]
+                a.X = nat.ptr(self.X) if s == 0 else None
+                a.Y = nat.ptr(self.Y) if s == K - 1 else None
+                a.params, a.opt_m, a.opt_v = nat.ptr(self.params[s]), nat.ptr(self.m[s]), nat.ptr(self.v[s])
+                a.step, a.status = nat.ptr(self.step[s]), nat.ptr(self.status[s])
+                a.loss_log = nat.ptr(self.loss_log) if s == K - 1 else None
+                a.act_in = self.act_buf[s]
+                a.act_out = self.act_buf[s + 1] if s + 1 < K else None
+                a.grad_in = self.grad_buf[s]
+                a.grad_out = self.grad_buf[s - 1] if s > 0 else None
+                a.dp_peers = nat.ptr(self._dp[s].peer_table) if self._dp[s] is not None else None
+                a.loss_log_cap = log_cap
+                a.n_steps = 1
+                a.timeout_us = int(timeout_us)
+                a.cache_data = 1
+                a.dp_world, a.dp_rank = self.world, self.rank
+                a.optim = nat.MODE_ADAM if self.optim.name == "adam" else nat.MODE_SGD
+                a.smp = geom.to_native()
+                a.hp = self.optim.hyper(spec.slope, 1.0 / self.world)
+                L.shape_id[j] = lib.dtp_split_shape_id(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
+                                                       int(ss.final_act), int(s == 0))
+            self._launch[dev] = L
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+
+    def _alloc(self, dev: torch.device, nbytes: int) -> int:
+        import ctypes
+
+        p = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            nat.check(self.lib.dtp_malloc_uncached(nbytes, ctypes.byref(p)), "dtp_malloc_uncached")
+        self._owned.append((dev.index, p.value))
+        return p.value
+
+    def train(self, n_steps: int) -> None:
+        """n_steps iterations: ONE persistent launch per GPU (its stages as co-resident
+        workgroups), asynchronous."""
+        if n_steps <= 0:
+            return
+        import ctypes
+
+        for dev, L in self._launch.items():
+            st = self.streams[dev]
+            st.wait_stream(torch.cuda.current_stream(dev))  # after any host-side state edits
+            for j in range(L.n):
+                L.stage[j].n_steps = n_steps
+            with torch.cuda.device(dev):
+                nat.check(self.lib.dtp_split_launch(ctypes.byref(L), nat.stream_ptr(st)), "dtp_split_launch")
+        self.t += n_steps
+
+    def _join(self):
+        for dev, st in self.streams.items():
+            torch.cuda.current_stream(dev).wait_stream(st)
+
+    def synchronize(self):
+        self._join()
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+        self.check_comm()
+
+    def check_comm(self):
+        self._join()
+        for s, st in enumerate(self.status):
+            w = st[:4].tolist()
+            if w[0]:
+                raise RuntimeError(f"layer-split link of stage {s} timed out at step {w[1] - 1} (neighbour stalled)")
+            if w[2]:
+                raise RuntimeError(f"data-parallel exchange of stage {s} timed out at step {w[3] - 1}")
+
+    def losses(self, t0: int, t1: int) -> torch.Tensor:
+        self._join()
+        cap = self.loss_log.shape[0]
+        t0 = max(t0, t1 - cap)
+        ids = torch.arange(t0, t1) % cap
+        return self.loss_log.index_select(0, ids.to(self.loss_log.device)).cpu()
+
+    def losses_async(self, t0: int, t1: int):
+        """Pinned copy of the losses of steps [t0, t1) queued behind the last stage's
+        work; ``.wait()`` returns [[loss], ...] (the fused engine's LossReadback)."""
+        from ..engine.fused_trainer import LossReadback
+
+        dev = self.devices[-1]
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_stream(self.streams[dev])
+        cap = self.loss_log.shape[0]
+        ids = torch.arange(max(t0, t1 - cap), t1) % cap
+        with torch.cuda.device(dev):
+            rows = self.loss_log.index_select(0, ids.to(dev)).view(-1, 1)
+            host = torch.empty(rows.shape, pin_memory=True)
+            host.copy_(rows, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+        return LossReadback(host, None, ev, self.rank)
+
+    def flat_params_cpu(self) -> torch.Tensor:
+        self._join()
+        return torch.cat([p.cpu() for p in self.params])
+
+    def state_dict(self) -> dict:
+        self._join()
+        return {"params": self.flat_params_cpu(), "m": torch.cat([m.cpu() for m in self.m]),
+                "v": torch.cat([v.cpu() for v in self.v]), "step": int(self.step[0].item()), "t": self.t}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self._join()
         o = 0
-        for p, n in zip(self.model.params, self.sizes):
-            self.buf[o:o + n].copy_(p.grad.reshape(-1), non_blocking=True)
+        for s, p in enumerate(self.params):
+            n = p.numel()
+            p.copy_(sd["params"][o:o + n])
+            self.m[s].copy_(sd["m"][o:o + n])
+            self.v[s].copy_(sd["v"][o:o + n])
+            self.step[s].fill_(int(sd["step"]))
             o += n
-        comm_util.all_reduce_(self.buf, self.group)
-        self.buf.mul_(1.0 / self.world)
-        o = 0
-        for p, n in zip(self.model.params, self.sizes):
-            p.grad.copy_(self.buf[o:o + n].view_as(p.grad), non_blocking=True)
-            o += n
+        self.t = int(sd["t"])
+
+    def close(self):
+        import ctypes
+
+        for s in range(len(self.devices)):
+            torch.cuda.synchronize(self.devices[s])
+        if self.world > 1 and dist.is_initialized():
+            comm_util.barrier(self.group)  # no peer is still writing into our buffers
+        for pb in self._dp:
+            if pb is not None:
+                pb.close()
+        self._dp = [None] * len(self.devices)
+        for dev_index, ptr in self._owned:
+            with torch.cuda.device(dev_index):
+                self.lib.dtp_free(ctypes.c_void_p(ptr))
+        self._owned = []

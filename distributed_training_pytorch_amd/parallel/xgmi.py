@@ -126,8 +126,10 @@ class XgmiAllReduce:
     (``csrc/xgmi_allreduce.hip``): FlatDDP's path for buckets up to ``cap``
     floats on a single node (W <= 8).
 
-    ``all_reduce_(t, scale)`` is asynchronous on the current stream; the epoch
-    advances on the host per call (calls are stream-ordered on every rank).
+    ``all_reduce_(t, scale)`` is asynchronous on the current stream.  The exchange
+    epochs are device counters the kernel advances itself (one per workgroup), so a
+    call captured in a hipGraph is a fresh exchange on every replay: the module
+    engine and the Trainer replay their whole step, xGMI buckets included.
     ``check()`` reads the sticky timeout word (one host sync) -- call it at
     logging/checkpoint boundaries, not per step.
     """
@@ -147,7 +149,10 @@ class XgmiAllReduce:
         self.rank = self.bufs.rank
         self.status = torch.zeros(16, dtype=torch.int32, device=device)
         self.timeout_us = int(timeout_us)
-        self.epoch = 0
+        # per-workgroup exchange counters, local to this rank: every rank counts the
+        # same sequence of calls from zero, so the k-th call carries epoch k everywhere
+        self.epochs = torch.zeros(max(1, self.lib.dtp_xgmi_allreduce_epoch_slots(self.cap)), dtype=torch.int32,
+                                  device=device)
 
     def all_reduce_(self, t: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
         if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
@@ -155,9 +160,8 @@ class XgmiAllReduce:
         n = t.numel()
         if n > self.cap:
             raise ValueError(f"{n} floats exceed the xGMI all-reduce capacity {self.cap}")
-        self.epoch += 1
         nat.check(self.lib.dtp_xgmi_allreduce(nat.ptr(t), n, self.cap, nat.ptr(self.bufs.peer_table), self.world,
-                                              self.rank, self.epoch & 0xFFFFFFFF, float(scale), nat.ptr(self.status),
+                                              self.rank, nat.ptr(self.epochs), float(scale), nat.ptr(self.status),
                                               self.timeout_us, nat.stream_ptr()), "dtp_xgmi_allreduce")
         return t
 

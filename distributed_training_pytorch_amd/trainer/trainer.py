@@ -383,7 +383,8 @@ class Trainer:
 
     def _batch_stepper(self, model, ddp, opts):
         """A CapturedStep replaying one batch's optimizer steps as a hipGraph, when the
-        run allows it: a GPU, one rank or RCCL buckets, and optimizers that can keep
+        run allows it: a GPU, buckets that can be captured (one rank, the in-kernel xGMI
+        all-reduce, or RCCL: ``FlatDDP.graph_safe``), and optimizers that can keep
         their step counts on the device (torch's ``capturable`` param-group flag).
 
         What a replay repeats is what the capture recorded: device work on the static
@@ -393,7 +394,7 @@ class Trainer:
         ``Trainer(use_graphs=False)`` runs every batch eagerly."""
         if not (self.use_graphs and self.device.type == "cuda"):
             return None, None
-        if ddp is not None and self.world_size > 1 and not (dist.get_backend() == "nccl" and ddp.comm == "rccl"):
+        if ddp is not None and not ddp.graph_safe():
             return None, None
         for opt in opts:
             if not all("capturable" in g for g in opt.param_groups) and not isinstance(opt, torch.optim.SGD):

@@ -132,3 +132,32 @@ def test_lightning_trainer_flat_optimizer_matches_torch_adam(tmp_path):
     st = ck["optimizer_states"][0]["state"]
     assert len(st) == 10 and all("exp_avg" in s and "exp_avg_sq" in s for s in st.values())
     assert all(float(s["step"]) == 64 for s in st.values())
+
+
+def test_demo_layer_split_fused_engine_on_gpu(tmp_path):
+    """The default engine of the layer-split demo: persistent stage kernels handing
+    activations / gradients over the peer-store links (both stages on the one GPU)."""
+    out = _run(["demo_one_model_multi_gpu.py", "--gpus_per_proc", "2", "--allow_shared_gpu", "--iters", "1000",
+                "--seed", "0", "--dry_run", "--no_progress", "--log_dir", str(tmp_path)])
+    assert "engine: fused layer split" in out, out[-2000:]
+    s = _summary(out)
+    assert s["engine"] == "split-fused" and s["stages"] == 2 and s["iters"] == 1000
+    assert 0.0 < s["final_loss"] < 4.0, s
+    assert s["us_per_step"] < 50.0, s
+
+
+def test_demo_layer_split_fused_resume_is_bit_exact(tmp_path):
+    import torch
+
+    base = ["demo_one_model_multi_gpu.py", "--gpus_per_proc", "2", "--allow_shared_gpu", "--seed", "3",
+            "--dry_run", "--no_progress", "--checkpoint_every", "50", "--log_every", "25"]
+    _run(base + ["--iters", "200", "--checkpoint_dir", str(tmp_path / "a"), "--log_dir", str(tmp_path / "la")])
+    _run(base + ["--iters", "100", "--checkpoint_dir", str(tmp_path / "b"), "--log_dir", str(tmp_path / "lb")])
+    out = _run(base + ["--iters", "200", "--checkpoint_dir", str(tmp_path / "b"), "--resume",
+                       "--log_dir", str(tmp_path / "lb2")])
+    assert "at iteration 100" in out
+    a = torch.load(tmp_path / "a" / "last.pt", weights_only=True)
+    b = torch.load(tmp_path / "b" / "last.pt", weights_only=True)
+    assert a["iteration"] == b["iteration"] == 200
+    for k in ("params", "m", "v"):
+        assert torch.equal(a[k], b[k]), k

@@ -208,3 +208,31 @@ def test_demo_cross_entropy_sgd_two_ranks(engine):
         outs[eng] = _summary(r.stdout)
     s = outs[engine]
     assert s["iters"] == 20 and all(0.0 < v < 5.0 for v in s["final_loss"])
+
+
+def test_layer_split_demo_two_ranks_resume_cpu(tmp_path):
+    """demo_one_model_multi_gpu.py on CPU (2 stages per process, 2 gloo ranks, the
+    autograd engine with per-device DDP buckets): checkpoint at 10, resume to 20 ends
+    bitwise where a straight 20-iteration run ends."""
+    import torch
+
+    def launch(ck, iters, resume):
+        args = [PY, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--master-addr",
+                "127.0.0.1", "--master-port", str(_free_port()), "demo_one_model_multi_gpu.py", "--torchrun",
+                *COMMON, "--iters", str(iters), "--checkpoint_dir", str(ck), "--checkpoint_every", "10",
+                "--log_dir", str(tmp_path / f"logs_{ck.name}_{iters}")]
+        r = _run(args + (["--resume"] if resume else []))
+        assert r.returncode == 0, r.stderr[-3000:]
+        return r
+
+    launch(tmp_path / "straight", 20, False)
+    launch(tmp_path / "split", 10, False)
+    r = launch(tmp_path / "split", 20, True)
+    assert "at iteration 10" in r.stdout and "split-module" in r.stdout
+    a = torch.load(tmp_path / "straight" / "last.pt", weights_only=True)
+    b = torch.load(tmp_path / "split" / "last.pt", weights_only=True)
+    for pa, pb in zip(a["params"], b["params"]):
+        assert torch.equal(pa, pb)
+    for oa, ob in zip(a["optim"], b["optim"]):
+        for k in ("m", "v", "step"):
+            assert torch.equal(oa[k], ob[k]), k

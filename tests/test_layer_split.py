@@ -8,12 +8,12 @@ from distributed_training_pytorch_amd.models.toy import ToyModel
 from distributed_training_pytorch_amd.parallel.layer_split import LayerSplitMLP, default_boundaries
 
 
-def _check(devs, bounds, mb, atol):
+def _check(devs, bounds, mb, atol, force_peer=False):
     torch.manual_seed(0)
     ref = ToyModel()
     x = torch.randn(96, 2)
     y = torch.randn(96, 1)
-    ls = LayerSplitMLP(ref.spec, devs, bounds, mb, ref.flat_params.detach())
+    ls = LayerSplitMLP(ref.spec, devs, bounds, mb, ref.flat_params.detach(), force_peer_buffers=force_peer)
     out = ls(x)
     loss = torch.nn.functional.mse_loss(out, y.to(out.device))
     loss.backward()
@@ -43,3 +43,60 @@ def test_layer_split_gpu(K, mb):
     n = torch.cuda.device_count()
     devs = [torch.device("cuda", s % n) for s in range(K)]
     _check(devs, None, mb, 2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [2, 3])
+def test_layer_split_peer_store_path_gpu(K):
+    """The hand-off through the stage kernel's epilogue peer store (out_peer) and the
+    next stage's gradient read from that separate buffer, forced on the one GPU."""
+    n = torch.cuda.device_count()
+    _check([torch.device("cuda", s % n) for s in range(K)], None, 1, 2e-5, force_peer=True)
+
+
+def _hybrid_rank(rank, world, steps):
+    """2 stages x 2 ranks (gloo): per-device buckets reduced from grad-ready hooks."""
+    from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig
+    from distributed_training_pytorch_amd.parallel.layer_split import LayerSplitDDP
+
+    torch.manual_seed(0)
+    ref = ToyModel()
+    ls = LayerSplitMLP(ref.spec, [torch.device("cpu")] * 2, None, 1, ref.flat_params.detach() * (1 + rank))
+    ddp = LayerSplitDDP(ls)  # broadcast: rank 1's different init is replaced by rank 0's
+    opts = [FlatOptimizer(p.data, p.grad, OptimConfig(lr=1e-2)) for p in ls.params]
+    g = torch.Generator().manual_seed(rank)
+    for _ in range(steps):
+        x, y = torch.randn(64, 2, generator=g), torch.randn(64, 1, generator=g)
+        ls.zero_grad()
+        torch.nn.functional.mse_loss(ls(x), y).backward()
+        ddp.finish()
+        for o in opts:
+            o.step()
+    return ls.flat_params_cpu(), ddp.comm
+
+
+def test_hybrid_split_ddp_per_device_buckets_cpu():
+    from .dist_utils import run_ranks
+
+    steps = 4
+    res = run_ranks(_hybrid_rank, 2, (steps,))
+    assert res[0][1] == "gloo"
+    assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
+    # reference: one process, gradient = mean of the two ranks' batch gradients
+    torch.manual_seed(0)
+    ref = ToyModel()
+    p = torch.nn.Parameter(ref.flat_params.detach().clone())
+    opt = torch.optim.Adam([p], lr=1e-2)
+    from distributed_training_pytorch_amd.ops.mlp import mlp_forward_ref
+
+    gens = [torch.Generator().manual_seed(r) for r in range(2)]
+    for _ in range(steps):
+        grads = []
+        for gen in gens:
+            x, y = torch.randn(64, 2, generator=gen), torch.randn(64, 1, generator=gen)
+            q = p.detach().clone().requires_grad_(True)
+            (gq,) = torch.autograd.grad(torch.nn.functional.mse_loss(mlp_forward_ref(q, ref.spec, x), y), q)
+            grads.append(gq)
+        p.grad = torch.stack(grads).mean(0)
+        opt.step()
+    torch.testing.assert_close(res[0][0], p.detach(), rtol=1e-5, atol=1e-6)

@@ -1,0 +1,109 @@
+"""The persistent layer-split engine (csrc/split_train.hip, parallel/layer_split.py:
+FusedLayerSplit): every stage one resident workgroup, activations / gradients handed
+over as epoch-tagged granules through the neighbour's receive buffer, weight
+gradients reduced over DP ranks in-kernel, Adam / SGD fused.  Stages share the one
+GPU here (distinct streams), so the same peer-store protocol runs through local
+uncached memory.  Ground truth: the UNSPLIT model trained with autograd +
+torch.optim (tests/ref_train.py)."""
+import time
+
+import pytest
+import torch
+
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.toy_data import ToyData
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
+from distributed_training_pytorch_amd.ops.optim import OptimConfig
+from distributed_training_pytorch_amd.parallel.layer_split import FusedLayerSplit
+
+from .dist_utils import run_ranks
+from .ref_train import torch_train
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _init(seed=5):
+    return torch.randn(TOY_SPEC.P, generator=torch.Generator().manual_seed(seed)) * 0.4
+
+
+def _engine(K, ocfg, bounds=None, batch=256, world=1, rank=0, seed=11):
+    ds = ToyData(n=512, seed=2)
+    geom = SamplerGeometry(n=512, world=world, rank=rank, batch=batch, seed=seed)
+    return FusedLayerSplit(TOY_SPEC, [DEV] * K, ds.X, ds.Y, geom, ocfg, _init(), boundaries=bounds), ds
+
+
+def _reference(ocfg, steps, batch=256, world=1, seed=11):
+    ds = ToyData(n=512, seed=2)
+    geoms = [SamplerGeometry(n=512, world=world, rank=r, batch=batch, seed=seed) for r in range(world)]
+    p, l = torch_train(TOY_SPEC, [_init()], ds.X, ds.Y, geoms, steps, ocfg, "mse")
+    return p[0], l[:, 0]
+
+
+@pytest.mark.parametrize("K,bounds", [(2, None), (3, None), (2, [(0, 2), (3, 4)]), (5, None)])
+@pytest.mark.parametrize("ocfg", [OptimConfig(lr=1e-2), OptimConfig("sgd", 5e-2, momentum=0.9)],
+                         ids=["adam", "sgd"])
+def test_fused_split_matches_unsplit_reference(K, bounds, ocfg):
+    steps = 12
+    eng, _ = _engine(K, ocfg, bounds)
+    eng.train(5)
+    eng.train(steps - 5)  # two launches: the stage state and the link epochs carry over
+    eng.synchronize()
+    rp, rl = _reference(ocfg, steps)
+    torch.testing.assert_close(eng.losses(0, steps), rl, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(eng.flat_params_cpu(), rp, rtol=1e-4, atol=2e-5)
+    assert [int(s.item()) for s in eng.step] == [steps] * K
+    eng.close()
+
+
+def test_fused_split_partial_batches_and_epochs():
+    """batch 100 over a 512-sample epoch: 5 full batches and a 12-sample tail per epoch."""
+    ocfg = OptimConfig(lr=1e-2)
+    steps = 14
+    eng, _ = _engine(2, ocfg, batch=100)
+    eng.train(steps)
+    eng.synchronize()
+    rp, rl = _reference(ocfg, steps, batch=100)
+    torch.testing.assert_close(eng.losses(0, steps), rl, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(eng.flat_params_cpu(), rp, rtol=1e-4, atol=2e-5)
+    eng.close()
+
+
+def test_fused_split_step_time():
+    """The reference's 2-GPU split at batch 256, both stages on one GPU: the whole
+    iteration (2 hand-offs + both stages' fwd/bwd/Adam) in microseconds, not the
+    ~0.44 ms of the host-driven autograd path."""
+    eng, _ = _engine(2, OptimConfig(lr=1e-3))
+    eng.train(50)
+    eng.synchronize()
+    n = 1000
+    t0 = time.perf_counter()
+    eng.train(n)
+    eng.synchronize()
+    us = (time.perf_counter() - t0) / n * 1e6
+    print(f"fused layer split (2 stages, one GPU): {us:.2f} us/step")
+    assert us < 40.0, us
+    eng.close()
+
+
+def _dp_rank(rank, world, steps):
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    eng, _ = _engine(2, OptimConfig(lr=1e-2), batch=128, world=world, rank=rank)
+    eng.train(steps)
+    eng.synchronize()
+    out = eng.flat_params_cpu(), eng.losses(0, steps)
+    eng.close()
+    return out
+
+
+def test_fused_split_with_data_parallel_two_ranks():
+    """Hybrid: 2 stages x 2 DP ranks, all four stage kernels on the one GPU; each
+    stage's gradient is reduced over the ranks inside its kernel."""
+    steps = 9
+    res = run_ranks(_dp_rank, 2, (steps,), timeout=300)
+    rp, rl = _reference(OptimConfig(lr=1e-2), steps, batch=128, world=2)
+    for r in range(2):
+        torch.testing.assert_close(res[r][1], rl, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(res[r][0], rp, rtol=1e-4, atol=2e-5)
+    assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
