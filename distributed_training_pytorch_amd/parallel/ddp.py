@@ -76,6 +76,7 @@ class FlatDDP(nn.Module):
             self._spans.append((lo, hi))
         self._pending = [0] * len(self._buckets)
         self._reduced = [False] * len(self._buckets)
+        self._ready: set = set()
         self._works = []
         self._callback_queued = False
         for p in params:
@@ -158,6 +159,14 @@ class FlatDDP(nn.Module):
             self._callback_queued = True
             self._pending = [len(b) for b in self._buckets]
             self._reduced = [False] * len(self._buckets)
+            self._ready = set()
+        # one notification per parameter per backward: a fused-grad parameter is
+        # reported by the kernel's grad-ready hook AND by torch's post-accumulate hook
+        # (which fires even for a None gradient); counting both would release a bucket
+        # before the last producing kernel was launched
+        if id(p) in self._ready:
+            return
+        self._ready.add(id(p))
         b = self._bucket_of[p]
         self._pending[b] -= 1
         if self._pending[b] == 0:

@@ -157,3 +157,35 @@ def test_trainer_resume_is_bit_exact(tmp_path):
     assert b_tr.current_epoch == ref_tr.current_epoch
     for (k, v), (k2, v2) in zip(ref.state_dict().items(), b.state_dict().items()):
         assert k == k2 and torch.equal(v, v2), k
+
+
+def test_post_accumulate_hooks_fire_for_none_grads_and_flatddp_counts_once():
+    """torch runs post-accumulate-grad hooks even for a None gradient, so a fused-grad
+    parameter (grad-ready hook + post-accumulate hook) notifies FlatDDP twice per
+    backward; a bucket must still wait for every parameter (regression: buckets were
+    released after half of them, before the last backward kernel ran)."""
+    from distributed_training_pytorch_amd.ops.gemm import _grad_ready, mark_fused_grad
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    class F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            ctx.w = w
+            return x * w
+
+        @staticmethod
+        def backward(ctx, g):
+            _grad_ready(ctx.w)  # a fused kernel "wrote" w.grad in place
+            return g, None
+
+    ws = [torch.nn.Parameter(torch.ones(3)) for _ in range(2)]
+    m = torch.nn.ParameterList(ws)
+    ddp = FlatDDP(m)
+    for w in ws:
+        mark_fused_grad(w)
+    reduced = []
+    orig = ddp._reduce_bucket
+    ddp._reduce_bucket = lambda b: (reduced.append((b, sum(len(ddp._ready) for _ in [0]))), orig(b))
+    x = torch.ones(3, requires_grad=True)
+    (F.apply(x, ws[0]).sum() + F.apply(x, ws[1]).sum()).backward()
+    assert reduced and reduced[0][1] == 2, reduced  # released only once both parameters reported
