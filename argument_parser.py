@@ -50,8 +50,9 @@ def build_parser(description: str | None = None) -> argparse.ArgumentParser:
     p.add_argument("--launch", choices=["persistent", "graph", "eager"], default="persistent")
     p.add_argument("--steps_per_launch", type=int, default=50,
                    help="iterations per kernel launch / graph (also the host logging granularity)")
-    p.add_argument("--sampler", choices=["device", "torch"], default="device",
-                   help="device: in-kernel Feistel shuffle; torch: exact DistributedSampler order")
+    p.add_argument("--sampler", choices=["torch", "device"], default="torch",
+                   help="torch: the reference's exact DistributedSampler order (randperm per epoch, read by "
+                        "the kernels from a device ring the host fills ahead); device: keyed Feistel shuffle")
     p.add_argument("--log_every", type=int, default=50)
     p.add_argument("--log_dir", type=str, default=None)
     p.add_argument("--project", type=str, default="distributed tester")

@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--sampler", choices=["torch", "device"], default="torch",
+                    help="torch: DistributedSampler's exact order (the reference loader); device: Feistel order")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32 = the reference's precision=32 (the headline); bf16 = bf16 matmul operands, "
                          "fp32 accumulation / master weights / Adam (BASELINE config 2)")
@@ -113,13 +115,15 @@ def main():
         torch.manual_seed(a.seed)
         init = [ToyModel().flat_params.detach().clone() for _ in range(2)]
         ecfg = EngineConfig(comm=a.comm, launch=a.launch, steps_per_launch=a.steps_per_launch,
-                            precision=a.precision)
+                            precision=a.precision, sampler=a.sampler)
         runner = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
         per_rank_batch = geom.batch_size_at(0)
         train = runner.train
         # the xGMI timeout word is checked right after the timed region (check_comm below)
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
-        cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm}
+        cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm,
+                    "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
+                    else "Feistel shuffle"}
 
     # the timed region is bracketed by an all-rank barrier + synchronize on both sides;
     # ranks of the in-kernel xGMI engine use the framework's device barrier (one xGMI

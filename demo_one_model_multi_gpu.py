@@ -18,7 +18,8 @@ TASKS_PER_NODE=1).  Two engines:
   activation into the next GPU, optional GPipe micro-batches (``--microbatches``),
   per-device DDP buckets reduced from grad-ready hooks (``LayerSplitDDP``).
 Configurations the persistent kernels do not cover (micro-batches, batch > 256,
-the exact torch sampler order) fall back to ``module`` with a printed reason.
+other losses) fall back to ``module`` with a printed reason.  Both engines draw the
+reference's exact DistributedSampler order by default (``--sampler torch``).
 Checkpoint / resume (``--checkpoint_dir --checkpoint_every --resume``) works for
 both.  Launch with torchrun (``--torchrun``) or plain srun exactly like demo.py.
 """
@@ -79,8 +80,6 @@ def _fused_reason(config, devs) -> str | None:
         return "GPipe micro-batches run on the autograd path"
     if config.batch_size > 256:
         return "per-rank batch > 256 (one lane per sample)"
-    if config.sampler == "torch":
-        return "exact torch sampler order (host-built indices)"
     if config.loss != "mse":
         return "the split stages implement the reference's MSE loss"
     return None
@@ -117,7 +116,8 @@ def main(argv=None):
     why = _fused_reason(config, devs)
     if why is None:
         try:
-            eng = FusedLayerSplit(toy.spec, devs, ds.X, ds.Y, geom, ocfg, toy.flat_params.detach(), bounds)
+            eng = FusedLayerSplit(toy.spec, devs, ds.X, ds.Y, geom, ocfg, toy.flat_params.detach(), bounds,
+                                  sampler=config.sampler)
         except NotImplementedError as e:
             why, eng = str(e), None
     if why is None:

@@ -44,6 +44,9 @@ class SamplerCfg(ctypes.Structure):
         ("steps_per_epoch", c_int),
         ("bits", c_int),
         ("seed", c_uint64),
+        ("perm", c_void_p),
+        ("perm_epochs", c_int),
+        ("pad_", c_int),
     ]
 
 
@@ -196,7 +199,7 @@ class GemmArgs(ctypes.Structure):
 DT_F32, DT_BF16 = 0, 1
 MODE_GRAD, MODE_ADAM, MODE_SGD, MODE_XGMI_ADAM, MODE_XGMI_SGD = 0, 1, 2, 3, 4
 LOSS_MSE, LOSS_CE = 0, 1
-SAMPLER_EXPLICIT, SAMPLER_DIST_SHUFFLE, SAMPLER_SEQUENTIAL, SAMPLER_DIST_NOSHUFFLE = 0, 1, 2, 3
+SAMPLER_EXPLICIT, SAMPLER_DIST_SHUFFLE, SAMPLER_SEQUENTIAL, SAMPLER_DIST_NOSHUFFLE, SAMPLER_TABLE = 0, 1, 2, 3, 4
 
 _lib = None
 _lock = threading.Lock()
@@ -223,6 +226,7 @@ def _declare(lib):
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
+        "dtp_randperm_fill": (c_int, [ctypes.c_ulonglong, c_int, c_longlong, c_int, c_void_p, c_int]),
         "dtp_split_launch": (c_int, [P(SplitLaunch), c_void_p]),
         "dtp_split_shape_id": (c_int, [c_int] * 6),
         "dtp_split_stage_supported": (c_int, [c_int] * 6),

@@ -84,11 +84,13 @@ struct SampleRegs {
 #else
 #define DTP_TRAIN_ATTR
 #endif
-// FAST: the common configuration fixed at compile time (MSE, batch <= 256, device
-// shuffle sampler, power-of-two dataset cached in LDS, 0 <= slope <= 1;
-// fast_path_ok() on the host):
-// the next step's sample gather is straight-line LDS code the scheduler can
-// interleave with the optimizer, and LeakyReLU is max(z, slope z).
+// FAST: the common configuration fixed at compile time (MSE, batch <= 256, the
+// SAMPLER_TABLE sampler -- the epoch permutations in a device ring the host fills
+// ahead, torch's exact DistributedSampler order by default --, dataset cached in LDS,
+// 0 <= slope <= 1; fast_path_ok() on the host): each lane's dataset index is loaded
+// from the ring a whole step before it is used, so the next step's sample gather
+// is straight-line LDS code the scheduler interleaves with the optimizer, and
+// LeakyReLU is max(z, slope z).
 template <class S, int MODE, bool PROF = false, bool FAST = false>
 __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
@@ -157,25 +159,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   auto gather = [&](int it_, const BatchPos& bp_, const uint32_t (&keys_)[4], int k, int bsz_) {
     SampleRegs<S> r;
     r.valid = k < bsz_;
-    if constexpr (FAST) {
-      // position in the padded list (padding repeats from the start), then the
-      // one-pass permutation of a power-of-two domain: no branches
-      int q = smp.rank + (bp_.start + k) * smp.world;
-      q = q >= smp.n ? q - smp.n : q;
-      int di = (int)feistel_permute_pow2((uint32_t)q, smp.bits, keys_);
-      di = r.valid ? di : 0;
-      static_for<0, S::IN>([&](auto IC) {
-        constexpr int i = decltype(IC)::value;
-        const float v = S::rnd(sm.data[di * S::IN + i]);
-        r.x[i] = r.valid ? v : 0.f;
-      });
-      static_for<0, S::OUT>([&](auto JC) {
-        constexpr int j = decltype(JC)::value;
-        const float v = j < ydim ? sm.data[yoff + di * ydim + j] : 0.f;
-        r.y[j] = r.valid ? v : 0.f;
-      });
-      return r;
-    }
     int di = 0;
     if (r.valid) di = explicit_idx ? a.idx[(size_t)it_ * smp.batch + k] : sample_index(smp, bp_, keys_, k);
     static_for<0, S::IN>([&](auto IC) {
@@ -197,7 +180,50 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     bp_.size = explicit_idx ? smp.batch : min(smp.batch, smp.num_samples - bp_.start);
     return bp_;
   };
-  SampleRegs<S> nxt = gather(0, batch_at(epoch, bi), keys, tid, batch_at(epoch, bi).size);
+  // FAST: this lane's dataset index of the step at (ep_, b_): the padded-list position
+  // (padding repeats from the start), looked up in the epoch's slot of the ring; -1
+  // past the batch.  The load is issued a step ahead of its use (fidx below).
+  auto fast_index = [&](int ep_, int b_) -> int {
+    const int start = b_ * smp.batch;
+    const int size = min(smp.batch, smp.num_samples - start);
+    int q = smp.rank + (start + tid) * smp.world;
+    q = q >= smp.n ? q - smp.n : q;
+    q = q < smp.n ? q : smp.n - 1;  // lanes past the batch: any in-range position
+    const int di = table_epoch(smp, ep_)[q];
+    return tid < size ? di : -1;
+  };
+  auto fast_gather = [&](int di) {
+    SampleRegs<S> r;
+    r.valid = di >= 0;
+    di = (unsigned)di < (unsigned)smp.n ? di : 0;  // never index LDS out of range
+    static_for<0, S::IN>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      const float v = S::rnd(sm.data[di * S::IN + i]);
+      r.x[i] = r.valid ? v : 0.f;
+    });
+    static_for<0, S::OUT>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      const float v = j < ydim ? sm.data[yoff + di * ydim + j] : 0.f;
+      r.y[j] = r.valid ? v : 0.f;
+    });
+    return r;
+  };
+  auto roll = [&](int& ep_, int& b_) {  // advance a (epoch, batch) cursor by one step, branch-free
+    const bool r_ = ++b_ == smp.steps_per_epoch;
+    b_ = r_ ? 0 : b_;
+    ep_ += r_ ? 1 : 0;
+  };
+  // FAST: the cursor and in-flight index of the step AFTER the next one to gather
+  int e2 = epoch, b2 = bi, fidx = 0;
+  SampleRegs<S> nxt;
+  if constexpr (FAST) {
+    const int fidx0 = fast_index(epoch, bi);
+    roll(e2, b2);
+    fidx = fast_index(e2, b2);
+    nxt = fast_gather(fidx0);  // waits for the first index (prologue only)
+  } else {
+    nxt = gather(0, batch_at(epoch, bi), keys, tid, batch_at(epoch, bi).size);
+  }
   // Adam bias-correction powers beta^t, carried in double like torch's host math
   // table entry e holds the scalars of step number t0 + base + e + 1
   auto fill_adam = [&](int base) {
@@ -365,18 +391,21 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     // (FAST: the gather is straight-line code in the optimizer's basic block; the
     // loss-log store, a branch of thread 0, comes after the update)
     const int lslot_now = lslot;
-    if constexpr (FAST) {  // branch-free: the epoch keys are re-derived every step (scalar unit)
-      const bool roll = ++bi == smp.steps_per_epoch;
-      bi = roll ? 0 : bi;
-      epoch += roll ? 1 : 0;
-      epoch_keys(smp, epoch, keys);
+    if constexpr (FAST) {
+      roll(epoch, bi);
     } else if (!explicit_idx && ++bi == smp.steps_per_epoch) {
       bi = 0;
       ++epoch;
       epoch_keys(smp, epoch, keys);
     }
     if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
-    if (FAST || it + 1 < a.n_steps) {  // FAST gathers past the last step too (harmless LDS reads)
+    if constexpr (FAST) {
+      // the next step's samples from the index loaded a step ago, then the load for the
+      // step after it (past the last step: an in-range table read, never used)
+      nxt = fast_gather(fidx);
+      roll(e2, b2);
+      fidx = fast_index(e2, b2);
+    } else if (it + 1 < a.n_steps) {
       const BatchPos bpn = batch_at(epoch, bi);
       nxt = gather(it + 1, bpn, keys, tid, bpn.size);
     }
@@ -499,8 +528,9 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   const int ydim = a.loss == DTP_LOSS_CE ? 1 : out;
   // n >= world: the FAST gather wraps a padded-list position with ONE subtraction of n
   // (positions stay below n + world - 1), where the generic sampler takes q % n
-  return a.cache_data && a.loss == DTP_LOSS_MSE && s.batch <= dtp::kBlock && s.mode == dtp::SAMPLER_DIST_SHUFFLE &&
-         s.bits >= 1 && s.bits < 31 && s.n == (1 << s.bits) && s.n >= s.world && s.n * (in + ydim) <= dtp::kDataCache &&
+  const bool ring = s.perm && s.perm_epochs > 0 && (s.perm_epochs & (s.perm_epochs - 1)) == 0;
+  return a.cache_data && a.loss == DTP_LOSS_MSE && s.batch <= dtp::kBlock && s.mode == dtp::SAMPLER_TABLE && ring &&
+         s.n >= s.world && s.n * (in + ydim) <= dtp::kDataCache &&
          a.hp.slope >= 0.f && a.hp.slope <= 1.f;
 }
 
@@ -532,6 +562,9 @@ int validate_train(const DtpTrainArgs* a, int mode) {
   if (a->smp.mode != dtp::SAMPLER_EXPLICIT && (a->smp.steps_per_epoch <= 0 || a->smp.num_samples <= 0))
     return set_err(-1, "bad sampler geometry");
   if (a->smp.mode == dtp::SAMPLER_EXPLICIT && !a->idx) return set_err(-1, "explicit sampler without indices");
+  if (a->smp.mode == dtp::SAMPLER_TABLE &&
+      (!a->smp.perm || a->smp.perm_epochs <= 0 || (a->smp.perm_epochs & (a->smp.perm_epochs - 1))))
+    return set_err(-1, "table sampler needs a power-of-two permutation ring");
   if (a->loss_log && a->loss_log_cap <= 0) return set_err(-1, "loss_log_cap must be positive");
   if (!a->params || !a->X || !a->Y || !a->step) return set_err(-1, "params, X, Y and step are required");
   if (mode == DTP_MODE_GRAD && !a->grad_out) return set_err(-1, "MODE_GRAD needs grad_out");
@@ -557,7 +590,7 @@ struct TrainEngine {
 template <class S>
 int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
   if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM))
-    return set_err(-2, "the profile instance is the FAST one: power-of-two cached dataset, shuffle sampler");
+    return set_err(-2, "the profile instance is the FAST one: cached dataset, SAMPLER_TABLE sampler");
   hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_ADAM, true, true>), dim3(a->n_models), dim3(dtp::kBlock), 0,
                      st, *a);
   return check_launch("mlp_train_kernel<prof>");

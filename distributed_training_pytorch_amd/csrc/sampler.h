@@ -23,6 +23,8 @@ enum SamplerMode : int {
   SAMPLER_DIST_SHUFFLE = 1,  // DistributedSampler(shuffle=True)
   SAMPLER_SEQUENTIAL = 2,  // DataLoader without sampler (every rank reads all of n in order)
   SAMPLER_DIST_NOSHUFFLE = 3,  // DistributedSampler(shuffle=False)
+  SAMPLER_TABLE = 4,       // DistributedSampler(shuffle=True) with the epoch permutations read from a
+                           // device ring `perm` filled by the host (randperm.hip: torch's exact order)
 };
 
 struct SamplerCfg {
@@ -35,7 +37,15 @@ struct SamplerCfg {
   int steps_per_epoch;
   int bits;         // Feistel domain = 2^bits >= n
   uint64_t seed;
+  const int* perm;  // SAMPLER_TABLE: [perm_epochs][n] ring, epoch e in slot e & (perm_epochs - 1)
+  int perm_epochs;  // power of two
+  int pad_;
 };
+
+// the permutation of epoch e in the SAMPLER_TABLE ring
+DTP_HD const int* table_epoch(const SamplerCfg& s, int epoch) {
+  return s.perm + (size_t)(epoch & (s.perm_epochs - 1)) * s.n;
+}
 
 DTP_HD uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
@@ -108,6 +118,7 @@ DTP_HD int sample_index(const SamplerCfg& s, const BatchPos& bp, const uint32_t 
   int q = s.rank + pos * s.world;  // position in the padded list
   if (q >= s.n) q %= s.n;           // padding repeats from the start
   if (s.mode == SAMPLER_DIST_SHUFFLE) return (int)feistel_permute((uint32_t)q, (uint32_t)s.n, s.bits, keys);
+  if (s.mode == SAMPLER_TABLE) return table_epoch(s, bp.epoch)[q];
   return q;
 }
 

@@ -259,3 +259,144 @@ class BatchIndexer:
             self._ep_idx = host.to(self.device, non_blocking=True)
             self._epoch = epoch
         return self._ep_idx[start:start + size]
+
+
+def randperm_torch(n: int, seed: int) -> list[int]:
+    """``torch.randperm(n, generator=torch.Generator().manual_seed(seed))`` (CPU): the
+    permutation DistributedSampler draws per epoch (with seed + epoch)."""
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g).tolist()
+
+
+class PermutationRing:
+    """Device ring of upcoming epoch permutations for the SAMPLER_TABLE sampler.
+
+    Slot ``e & (epochs-1)`` holds epoch e's permutation of [0, n): torch's exact
+    DistributedSampler order (``kind="torch"``: ``randperm(n)`` seeded with seed+epoch,
+    generated by the native MT19937 replica ``csrc/randperm.hip`` on host threads) or
+    the keyed Feistel permutation of the in-kernel device sampler (``kind="feistel"``).
+    The fused train kernel reads a lane's dataset index from the ring a step ahead,
+    so the reference's exact sample order costs no host work per step.
+
+    ``ensure(e_lo, e_hi)`` makes epochs [e_lo, e_hi] resident before a launch that
+    reads them (one stream-ordered H2D copy of the missing epochs); a background thread
+    keeps the next block generated in pinned memory, so long runs refill from a ready
+    buffer.  The constructor fills the whole ring: a short run never refills."""
+
+    def __init__(self, geom: SamplerGeometry, device: torch.device, kind: str = "torch", epochs: int | None = None,
+                 budget_ints: int = 1 << 24):
+        import threading
+
+        if kind not in ("torch", "feistel"):
+            raise ValueError(f"permutation kind {kind!r}: torch or feistel")
+        self.geom = geom
+        self.n = geom.n
+        self.kind = kind
+        self.device = torch.device(device)
+        if epochs is None:
+            epochs = max(2, min(8192, budget_ints // max(self.n, 1)))
+        self.E = 1 << (int(epochs).bit_length() - 1)  # power of two
+        self.table = torch.empty(self.E, self.n, dtype=torch.int32, device=self.device)
+        self.lo, self.hi = 0, -1  # resident epochs [lo, hi]
+        self._lock = threading.Lock()
+        self._ahead = None  # (e0, count, pinned host tensor) of a prefetched block
+        self._thread = None
+        self._keep = []  # pinned buffers of in-flight copies
+        self._write(0, self._generate(0, self.E))
+
+    # ---------------------------------------------------------------- generation
+    def _generate(self, e0: int, count: int) -> torch.Tensor:
+        host = torch.empty(count, self.n, dtype=torch.int32, pin_memory=self.device.type == "cuda")
+        if self.kind == "torch":
+            self._fill_torch(e0, count, host)
+        else:
+            for k in range(count):
+                keys = epoch_keys(self.geom.seed, e0 + k)
+                host[k] = torch.from_numpy(
+                    feistel_permute_array(np.arange(self.n), self.n, self.geom.bits, keys).astype(np.int32))
+        return host
+
+    def _fill_torch(self, e0: int, count: int, host: torch.Tensor) -> None:
+        try:
+            from .. import _native as nat
+
+            lib = nat.load()
+        except Exception:  # no native library (CPU-only checkouts): torch's own generator
+            lib = None
+        if lib is not None:
+            import os
+
+            threads = min(16, os.cpu_count() or 1)  # the box's CPU share per GPU
+            nat.check(lib.dtp_randperm_fill(self.geom.seed & 0xFFFFFFFFFFFFFFFF, self.n, e0, count,
+                                            host.data_ptr(), threads), "dtp_randperm_fill")
+            return
+        for k in range(count):
+            host[k] = torch.tensor(randperm_torch(self.n, self.geom.seed + e0 + k), dtype=torch.int32)
+
+    def _prefetch(self, e0: int, count: int) -> None:
+        import threading
+
+        def work():
+            blk = self._generate(e0, count)
+            with self._lock:
+                self._ahead = (e0, count, blk)
+
+        self._thread = threading.Thread(target=work, daemon=True)
+        self._thread.start()
+
+    # ---------------------------------------------------------------- residency
+    def _write(self, e0: int, host: torch.Tensor) -> None:
+        """Copy epochs [e0, e0 + len(host)) into their slots (stream-ordered)."""
+        count = host.shape[0]
+        s0 = e0 & (self.E - 1)
+        first = min(count, self.E - s0)
+        self.table[s0:s0 + first].copy_(host[:first], non_blocking=True)
+        if first < count:
+            self.table[:count - first].copy_(host[first:], non_blocking=True)
+        self._keep = [host]
+        self.hi = max(self.hi, e0 + count - 1)
+        self.lo = max(self.lo, self.hi - self.E + 1)
+
+    def ensure(self, e_lo: int, e_hi: int) -> None:
+        if e_hi - e_lo + 1 > self.E:
+            raise ValueError(f"a launch spanning {e_hi - e_lo + 1} epochs exceeds the {self.E}-epoch ring: "
+                             "launch fewer steps at a time")
+        if e_lo < self.lo:  # rewound (e.g. a checkpoint restored an earlier step)
+            self.lo, self.hi = e_lo, e_lo - 1
+        if e_hi > self.hi:
+            need0 = max(self.hi + 1, e_lo)
+            blk = None
+            if self._thread is not None:
+                self._thread.join()
+                self._thread = None
+                with self._lock:
+                    ahead, self._ahead = self._ahead, None
+                if ahead is not None and ahead[0] <= need0 and ahead[0] + ahead[1] - 1 >= e_hi:
+                    blk = ahead[2][need0 - ahead[0]:]
+            # never evict an epoch this launch still reads: at most e_lo + E - 1
+            cap = e_lo + self.E - 1
+            if blk is None:
+                need_hi = min(max(e_hi, need0 + self.E // 2 - 1), cap)
+                blk = self._generate(need0, need_hi - need0 + 1)
+            blk = blk[:cap - need0 + 1]
+            if need0 > self.hi + 1:
+                self.lo, self.hi = need0, need0 - 1
+            self._write(need0, blk)
+        # keep the next block generating while the GPU works through this one
+        if self._thread is None and self._ahead is None and self.hi - e_hi < self.E // 2:
+            self._prefetch(self.hi + 1, self.E // 2)
+
+    def native(self, cfg):
+        """Point a SamplerCfg (``SamplerGeometry.to_native()``) at the ring."""
+        from .. import _native as nat
+
+        cfg.mode = nat.SAMPLER_TABLE
+        cfg.perm = self.table.data_ptr()
+        cfg.perm_epochs = self.E
+        return cfg
+
+    def epochs_of_steps(self, t0: int, t1: int) -> tuple[int, int]:
+        """Epochs read by steps [t0, t1] (the kernel also prefetches step t1 + 1)."""
+        spe = self.geom.steps_per_epoch
+        return t0 // spe, (t1 + 1) // spe

@@ -29,7 +29,7 @@ import torch.distributed as dist
 
 from .. import _native as nat
 from ..parallel import comm_util
-from ..data.sampler import EpochIndexStream, SamplerGeometry
+from ..data.sampler import SAMPLER_DIST_SHUFFLE, EpochIndexStream, PermutationRing, SamplerGeometry
 from ..ops.mlp import MlpSpec, mlp_forward_ref
 from ..ops.optim import OptimConfig, adam_update_ref, flat_optimizer_step, sgd_update_ref
 
@@ -39,7 +39,10 @@ class EngineConfig:
     comm: str = "auto"           # auto | none | rccl | xgmi | gloo
     launch: str = "persistent"   # persistent | graph | eager
     steps_per_launch: int = 1000  # persistent: iterations per kernel; graph: launches per graph
-    sampler: str = "device"      # device (in-kernel Feistel) | torch (exact DistributedSampler order)
+    # torch: the reference's exact DistributedSampler order (randperm(n) seeded with
+    # seed+epoch), device: the keyed Feistel order; both read from a device ring of
+    # upcoming epoch permutations (data/sampler.py: PermutationRing, SAMPLER_TABLE)
+    sampler: str = "torch"
     loss: str = "mse"            # mse | ce
     log_cap: int = 1 << 16
     cache_data: bool = True
@@ -90,6 +93,7 @@ class FusedTrainer:
         self._dev_index = self.device.index if self.device.index is not None else (
             torch.cuda.current_device() if self.device.type == "cuda" else -1)
         self._xgmi = None
+        self._ring = None
         self.comm = self._resolve_comm()
         # DDP construction semantics: every rank starts from rank 0's weights
         if self.world > 1:
@@ -107,6 +111,10 @@ class FusedTrainer:
                 raise NotImplementedError(f"no fused train kernel for {spec}")
             # scalar-weight workspace of the fused step (csrc/mlp_scalar.h), scratch
             self.wsp = torch.zeros(n_models * ws, dtype=torch.float32, device=dev)
+            if geom.mode == SAMPLER_DIST_SHUFFLE:
+                if self.cfg.sampler not in ("torch", "device"):
+                    raise ValueError(f"sampler {self.cfg.sampler!r}: torch or device")
+                self._ring = PermutationRing(geom, dev, kind="torch" if self.cfg.sampler == "torch" else "feistel")
         if self.comm == "xgmi":
             self._setup_xgmi()
 
@@ -239,6 +247,8 @@ class FusedTrainer:
     def _train_args(self, n_steps: int, mode: int, idx: torch.Tensor | None, batch_override: int | None = None):
         g = self.geom
         smp = g.to_native()
+        if self._ring is not None:
+            self._ring.native(smp)
         if idx is not None:
             smp.mode = nat.SAMPLER_EXPLICIT
             smp.batch = batch_override or g.batch
@@ -274,30 +284,38 @@ class FusedTrainer:
             G = max(1, min(self.cfg.steps_per_launch, 64))
             while remaining > 0:
                 k = G if remaining >= G else 1
+                self._ensure_epochs(k)
                 self._rccl_steps(k)
                 remaining -= k
             return
         remaining = n_steps
         while remaining > 0:
-            if self.cfg.sampler == "torch":
-                k = self._explicit_chunk(remaining)
-                self._launch_explicit(k)
-            elif self.cfg.launch == "persistent":
+            if self.cfg.launch == "persistent":
                 k = min(remaining, self.cfg.steps_per_launch)
+                self._ensure_epochs(k)
                 self._run_engine(k)
             elif self.cfg.launch == "graph":
                 G = self.cfg.steps_per_launch
                 if remaining >= G:
+                    self._ensure_epochs(G)
                     self._graph_launch(G)
                     k = G
                 else:  # a tail shorter than the captured graph: one-step launches via the native executor
                     k = 1
+                    self._ensure_epochs(1)
                     self._run_engine(1)
             else:
                 k = 1
+                self._ensure_epochs(1)
                 self._run_engine(1)
             remaining -= k
             self.t += k
+
+    def _ensure_epochs(self, k: int) -> None:
+        """The permutation ring holds every epoch the next k steps read (usually a no-op:
+        the ring is filled ahead; a refill is one stream-ordered copy)."""
+        if self._ring is not None:
+            self._ring.ensure(*self._ring.epochs_of_steps(self.t, self.t + k - 1))
 
     def _run_engine(self, k: int):
         """k iterations in one persistent launch through the native executor: the
@@ -336,36 +354,11 @@ class FusedTrainer:
             self._graphs[key] = h
         nat.check(lib.dtp_graph_launch(ctypes.c_void_p(h), nat.stream_ptr()), "dtp_graph_launch")
 
-    def _explicit_chunk(self, remaining: int) -> int:
-        # steps with the same batch size can share one launch
-        k = 0
-        b0 = self.geom.batch_size_at(self.t)
-        while k < min(remaining, self.cfg.steps_per_launch) and self.geom.batch_size_at(self.t + k) == b0:
-            k += 1
-        return k
-
-    def _launch_explicit(self, k: int):
-        b0 = self.geom.batch_size_at(self.t)
-        rows = [self._idx_stream.indices(self.t + i) for i in range(k)]
-        idx = torch.tensor(rows, dtype=torch.int32).pin_memory().to(self.device, non_blocking=True)
-        self._launch(k, idx, b0)
-        self._keepalive = idx
-
     def _rccl_steps(self, k: int):
         """k iterations of grad kernel -> RCCL all-reduce -> flat optimizer; with
         rccl_graph, all k captured in ONE hipGraph (one host replay per k steps: a
         replay costs ~10 us of host time, more than the step itself)."""
         lib = nat.load()
-        if self.cfg.sampler == "torch":
-            # exact DistributedSampler order: host-built indices, one eager step each
-            for _ in range(k):
-                b = self.geom.batch_size_at(self.t)
-                idx = torch.tensor([self._idx_stream.indices(self.t)], dtype=torch.int32).pin_memory()
-                idx = idx.to(self.device, non_blocking=True)
-                self._rccl_body(lib, idx, b)
-                self._keepalive = idx
-                self.t += 1
-            return
         if self.cfg.rccl_graph and self.comm == "rccl":
             g = self._graphs.get(("rccl", k))
             if g is None:

@@ -314,7 +314,7 @@ class FusedLayerSplit:
 
     def __init__(self, spec: MlpSpec, devices: list[torch.device], X: torch.Tensor, Y: torch.Tensor, geom,
                  optim, init_flat: torch.Tensor, boundaries: list[tuple[int, int]] | None = None, group=None,
-                 timeout_us: int = 2_000_000, log_cap: int = 1 << 16):
+                 timeout_us: int = 2_000_000, log_cap: int = 1 << 16, sampler: str = "torch"):
         import ctypes
 
         from ..ops.optim import OptimConfig
@@ -371,6 +371,15 @@ class FusedLayerSplit:
             for s, (ss, dev) in enumerate(zip(self.stage_specs, self.devices)):
                 with torch.cuda.device(dev):
                     self._dp[s] = PeerBuffers(int(lib.dtp_xgmi_fused_buffer_bytes(ss.P, 1, self.world)), dev, group)
+        # sample order: the stages that gather (first: inputs, last: targets) read the
+        # epoch permutations from a ring on their own GPU (torch's exact order by default)
+        from ..data.sampler import SAMPLER_DIST_SHUFFLE, PermutationRing
+
+        self.rings: dict = {}
+        if geom.mode == SAMPLER_DIST_SHUFFLE:
+            kind = "torch" if sampler == "torch" else "feistel"
+            for dev in {self.devices[0], self.devices[-1]}:
+                self.rings[dev] = PermutationRing(geom, dev, kind=kind)
         # the stages that share a GPU run as ONE launch (one workgroup each: co-resident
         # by construction); one stream per GPU
         self.groups: dict[torch.device, list[int]] = {}
@@ -404,6 +413,8 @@ class FusedLayerSplit:
                 a.dp_world, a.dp_rank = self.world, self.rank
                 a.optim = nat.MODE_ADAM if self.optim.name == "adam" else nat.MODE_SGD
                 a.smp = geom.to_native()
+                if dev in self.rings and (s == 0 or s == K - 1):
+                    self.rings[dev].native(a.smp)
                 a.hp = self.optim.hyper(spec.slope, 1.0 / self.world)
                 L.shape_id[j] = lib.dtp_split_shape_id(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
                                                        int(ss.final_act), int(s == 0))
@@ -427,6 +438,8 @@ class FusedLayerSplit:
             return
         import ctypes
 
+        for ring in self.rings.values():
+            ring.ensure(*ring.epochs_of_steps(self.t, self.t + n_steps - 1))
         for dev, L in self._launch.items():
             st = self.streams[dev]
             st.wait_stream(torch.cuda.current_stream(dev))  # after any host-side state edits

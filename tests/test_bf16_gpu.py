@@ -11,7 +11,7 @@ import sys
 import pytest
 import torch
 
-from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry
 from distributed_training_pytorch_amd.data.toy_data import ToyData
 from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, fused_mlp, mlp_forward_ref_bf16, unflatten
@@ -73,7 +73,7 @@ def test_fused_trainer_bf16_tracks_fp32_reference(launch):
     tr.train(steps)
     tr.synchronize()
     got = tr.losses(0, steps)
-    _, ref = torch_train(TOY_SPEC, init, ds.X, ds.Y, [geom], steps, OptimConfig(lr=1e-2), "mse")
+    _, ref = torch_train(TOY_SPEC, init, ds.X, ds.Y, [EpochIndexStream(geom)], steps, OptimConfig(lr=1e-2), "mse")
     rel = ((got - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
     assert rel < 5e-2, rel  # bf16 tolerance against the fp32 run
     assert not torch.equal(got, ref)  # and not silently the fp32 kernel

@@ -3,7 +3,7 @@ gradient averaging == single-process average of the per-rank batch gradients,
 replica consistency, global mean loss."""
 import torch
 
-from distributed_training_pytorch_amd.data.sampler import SamplerGeometry, torch_distributed_indices
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry, torch_distributed_indices
 from distributed_training_pytorch_amd.data.toy_data import ToyData
 from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, mlp_forward_ref
@@ -30,7 +30,8 @@ def _rank_fn(rank, world, steps):
 
 def _reference(world, steps):
     ds = ToyData(n=512, seed=1)
-    geoms = [SamplerGeometry(n=512, world=world, rank=r, batch=128, seed=3) for r in range(world)]
+    # the engine's default sampler is the reference's exact DistributedSampler order
+    geoms = [EpochIndexStream(SamplerGeometry(n=512, world=world, rank=r, batch=128, seed=3)) for r in range(world)]
     params = torch.stack(_init(100))
     m = torch.zeros_like(params)
     v = torch.zeros_like(params)
@@ -143,7 +144,7 @@ def test_loss_and_optimizer_options_gloo_dp(loss, ocfg):
     res = run_ranks(_loss_optim_rank, 2, (loss, ocfg, steps))
     spec = MlpSpec(2, 10, 5, 4) if loss == "ce" else TOY_SPEC
     ds = ToyData(n=512, seed=3, classes=4 if loss == "ce" else 0)
-    geoms = [SamplerGeometry(n=512, world=2, rank=r, batch=128, seed=11) for r in range(2)]
+    geoms = [EpochIndexStream(SamplerGeometry(n=512, world=2, rank=r, batch=128, seed=11)) for r in range(2)]
     g = torch.Generator().manual_seed(100)
     init = [torch.randn(spec.P, generator=g) * 0.4 for _ in range(2)]
     rp, rl = torch_train(spec, init, ds.X, ds.Y, geoms, steps, ocfg, loss)

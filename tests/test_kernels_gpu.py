@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from distributed_training_pytorch_amd import _native as nat
-from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry
 from distributed_training_pytorch_amd.data.toy_data import ToyData
 from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, MlpSpec, mlp_forward_ref, stage_backward, stage_forward
@@ -126,7 +126,7 @@ def test_fused_trainer_matches_reference(launch):
     steps = 14  # graph: three 4-step graphs, then a 2-step tail of one-step launches
     tr.train(steps)
     tr.synchronize()
-    ref_p, ref_l = _ref_train(TOY_SPEC, torch.stack(init), X, Y, geom, steps, cfg)
+    ref_p, ref_l = _ref_train(TOY_SPEC, torch.stack(init), X, Y, EpochIndexStream(geom), steps, cfg)
     torch.testing.assert_close(tr.losses(0, steps), ref_l, rtol=2e-4, atol=1e-5)
     torch.testing.assert_close(tr.params, ref_p, rtol=1e-3, atol=2e-5)
     assert tr.step_ctr.tolist() == [steps, steps]
@@ -147,7 +147,7 @@ def test_fused_trainer_large_dataset(n, cache):
     steps = 10
     tr.train(steps)
     tr.synchronize()
-    ref_p, ref_l = _ref_train(TOY_SPEC, torch.stack(init), X, Y, geom, steps, cfg)
+    ref_p, ref_l = _ref_train(TOY_SPEC, torch.stack(init), X, Y, EpochIndexStream(geom), steps, cfg)
     torch.testing.assert_close(tr.losses(0, steps), ref_l, rtol=2e-4, atol=1e-5)
     torch.testing.assert_close(tr.params, ref_p, rtol=1e-3, atol=2e-5)
     tr.close()
@@ -156,7 +156,7 @@ def test_fused_trainer_large_dataset(n, cache):
 _FAST_SCRIPT = r"""
 import sys, torch
 sys.path.insert(0, {root!r})
-from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry
 from distributed_training_pytorch_amd.data.toy_data import ToyData
 from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC

@@ -56,3 +56,44 @@ def test_loss_ring_reduces_chunks_like_per_step_all_reduce():
         assert [s for s, _ in got] == list(range(7))
         for s, (vx, vy) in got:
             assert vx == (s + s + 1) / 2 and vy == 5.0
+
+
+def test_native_randperm_is_torch_randperm():
+    """csrc/randperm.hip (MT19937 + Fisher-Yates, host threads) reproduces
+    torch.randperm(n, generator seeded with seed + epoch) bit for bit -- the order the
+    fused kernels read from the permutation ring by default."""
+    import torch
+
+    from distributed_training_pytorch_amd import _native as nat
+
+    lib = nat.load()
+    for n, seed, e0, ne in [(512, 0, 0, 5), (512, 7, 1000, 3), (100, 3, 0, 4), (4096, 12345, 17, 2), (3, 0, 0, 8)]:
+        out = torch.empty(ne, n, dtype=torch.int32)
+        nat.check(lib.dtp_randperm_fill(seed, n, e0, ne, out.data_ptr(), 4), "dtp_randperm_fill")
+        for k in range(ne):
+            g = torch.Generator()
+            g.manual_seed(seed + e0 + k)
+            assert out[k].tolist() == torch.randperm(n, generator=g).tolist(), (n, seed, e0 + k)
+
+
+def test_permutation_ring_cpu_refill_and_order():
+    """PermutationRing: slot e & (E-1) holds epoch e; ensure() refills across the ring's
+    wrap and after a rewind; the padded per-rank positions read through it give exactly
+    DistributedSampler's indices."""
+    import torch
+
+    from distributed_training_pytorch_amd.data.sampler import (PermutationRing, SamplerGeometry,
+                                                               torch_distributed_indices)
+
+    g = SamplerGeometry(n=100, world=3, rank=1, batch=16, seed=4)
+    ring = PermutationRing(g, torch.device("cpu"), epochs=8)
+    assert ring.E == 8 and (ring.lo, ring.hi) == (0, 7)
+    for lo, hi in [(0, 3), (6, 12), (20, 27), (2, 5)]:
+        ring.ensure(lo, hi)
+        for e in range(lo, hi + 1):
+            perm = ring.table[e & 7].tolist()
+            ref = torch_distributed_indices(100, 3, 1, e, seed=4)
+            pos = [(1 + j * 3) % 100 for j in range(g.num_samples)]
+            assert [perm[q] for q in pos] == ref, e
+    if ring._thread is not None:
+        ring._thread.join()

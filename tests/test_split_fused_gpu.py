@@ -10,7 +10,7 @@ import time
 import pytest
 import torch
 
-from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry
 from distributed_training_pytorch_amd.data.toy_data import ToyData
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
 from distributed_training_pytorch_amd.ops.optim import OptimConfig
@@ -35,7 +35,9 @@ def _engine(K, ocfg, bounds=None, batch=256, world=1, rank=0, seed=11):
 
 def _reference(ocfg, steps, batch=256, world=1, seed=11):
     ds = ToyData(n=512, seed=2)
-    geoms = [SamplerGeometry(n=512, world=world, rank=r, batch=batch, seed=seed) for r in range(world)]
+    # the engine's default order: the reference's DistributedSampler (randperm per epoch)
+    geoms = [EpochIndexStream(SamplerGeometry(n=512, world=world, rank=r, batch=batch, seed=seed))
+             for r in range(world)]
     p, l = torch_train(TOY_SPEC, [_init()], ds.X, ds.Y, geoms, steps, ocfg, "mse")
     return p[0], l[:, 0]
 

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 9
 
 
-def _gpu_rank(rank, world, comm, steps, launch, sampler="device"):
+def _gpu_rank(rank, world, comm, steps, launch, sampler="torch"):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ds = ToyData(n=512, seed=1)
