@@ -85,7 +85,7 @@ class TrainArgs(ctypes.Structure):
         ("cache_data", c_int),
         ("timeout_us", c_int),
         ("bf16", c_int),
-        ("pad_", c_int),
+        ("host_t0", c_int),
         ("smp", SamplerCfg),
         ("hp", Hyper),
     ]
@@ -221,7 +221,7 @@ def _declare(lib):
         "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
         "dtp_xgmi_fused_buffer_bytes": (c_longlong, [c_int, c_int, c_int]),
         "dtp_train_engine_create": (c_void_p, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
-        "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_void_p]),
+        "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_int, c_void_p]),
         "dtp_train_engine_destroy": (None, [c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),

@@ -44,7 +44,7 @@ struct DtpTrainArgs {
   int cache_data;       // stage the dataset in LDS (persistent multi-step runs)
   int timeout_us;       // bound on every cross-GPU spin (xGMI)
   int bf16;             // bf16 compute instance (fp32 master weights / Adam), toy shapes
-  int pad_;
+  int host_t0;          // >= 0: the step number of the first step (= the device counters), else read them
   dtp::SamplerCfg smp;
   DtpHyper hp;
 };

@@ -154,10 +154,13 @@ DTP_DEV float* pipe_stage(const PipeBwdCtx<S>& c, const float (&h)[S::NL + 1][16
   constexpr int I = S::din(l), O = S::dout(l);
   constexpr bool packed = SC::PACK && (l == 0 || l == S::NL - 1);
   float* stg = packed ? c.stg_pack : c.stg_hid;
-  stage_cols<O>(stg, c.lane, SC::rowoff(l), dz);
-  if constexpr (l == S::NL - 1) stage_one(stg, c.lane, SC::lossrow(), c.lpart);
-  stage_cols<I>(stg + kStgArr, c.lane, SC::coloff(l), h[l]);
-  stage_one(stg + kStgArr, c.lane, SC::coloff(l) + I, 1.f);
+  using TK = TileKind<S>;
+  TK::template cols<O>(stg, c.lane, SC::rowoff(l), dz);
+  // the batch loss rides in a free row of the output tile (f32 only: a bf16 operand
+  // would round it; the bf16 instance sums the loss with a wave reduction instead)
+  if constexpr (l == S::NL - 1 && !S::BF) stage_one(stg, c.lane, SC::lossrow(), c.lpart);
+  TK::template cols<I>(stg + kStgArr, c.lane, SC::coloff(l), h[l]);
+  TK::one(stg + kStgArr, c.lane, SC::coloff(l) + I, 1.f);
   return stg;
 }
 
@@ -170,11 +173,13 @@ DTP_DEV void pipe_bwd_layer(const PipeBwdCtx<S>& c, const BBlk<S, l>& B, const f
   using SC = Scal<S>;
   constexpr int I = S::din(l), O = S::dout(l), NQ = BBlk<S, l>::NQ;
   constexpr bool packed = SC::PACK && (l == 0 || l == S::NL - 1);
+  using TK = TileKind<S>;
+  constexpr int NK = TK::NK;
   float* stg = pipe_stage<S, l>(c, h, dz);
-  TileOps to;
+  typename TK::Ops to;
   if constexpr (!packed) {
     __builtin_amdgcn_wave_barrier();
-    to = tile_ops(stg, stg + kStgArr, c.lane);
+    to = TK::ops(stg, stg + kStgArr, c.lane);
   }
   f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 a0 = acc[SC::tile(l)];
@@ -185,7 +190,7 @@ DTP_DEV void pipe_bwd_layer(const PipeBwdCtx<S>& c, const BBlk<S, l>& B, const f
   static_for<0, O>([&](auto JC) {
     constexpr int j = decltype(JC)::value;
     if constexpr (!packed && j >= J0) {
-      constexpr int k0 = 16 * (j - J0) / (O - J0), k1 = 16 * (j - J0 + 1) / (O - J0);
+      constexpr int k0 = NK * (j - J0) / (O - J0), k1 = NK * (j - J0 + 1) / (O - J0);
       static_for<k0, k1>([&](auto KC) { tile_kstep<decltype(KC)::value>(to, a0, a1); });
     }
     const f32x2 d = f32x2{dz[j], dz[j]};
@@ -224,7 +229,7 @@ DTP_DEV void pipe_bwd_rest(const PipeBwdCtx<S>& c, const BBlk<S, l>& B, const fl
     float* stg = pipe_stage<S, 0>(c, h, dz);
     if constexpr (!SC::PACK) {
       __builtin_amdgcn_wave_barrier();
-      acc[SC::tile(0)] = wave_outer_acc(stg, stg + kStgArr, acc[SC::tile(0)], c.lane);
+      acc[SC::tile(0)] = TileKind<S>::outer(stg, stg + kStgArr, acc[SC::tile(0)], c.lane);
     }
   }
 }
@@ -241,7 +246,7 @@ DTP_DEV void pipe_backward(const PipeBwdCtx<S>& c, const BBlk<S, S::NL - 1>& bt,
   pipe_bwd_rest<S, S::NL - 2>(c, bt2, h, dz, acc);
   if constexpr (SC::PACK) {
     __builtin_amdgcn_wave_barrier();
-    acc[0] = wave_outer_acc(c.stg_pack, c.stg_pack + kStgArr, acc[0], c.lane);
+    acc[0] = TileKind<S>::outer(c.stg_pack, c.stg_pack + kStgArr, acc[0], c.lane);
     __builtin_amdgcn_wave_barrier();
   }
 }

@@ -14,6 +14,8 @@
 // a global workspace) measured slower than the LDS blocks and was removed in round 2
 // (docs/perf_notes.md, v3); the workspace size query (WS) stays as the shape check.
 #pragma once
+#include <type_traits>
+
 #include "mlp_core.h"
 
 namespace dtp {
@@ -255,5 +257,82 @@ DTP_DEV void stage_cols(float* __restrict__ buf, int lane, int c0, const float (
 DTP_DEV void stage_one(float* __restrict__ buf, int lane, int col, float v) {
   buf[(lane & 3) * kStgQ + (lane >> 2) + col * 16] = v;
 }
+
+// ---- bf16 compute (Stage<..., BF = true>): the dW tiles on v_mfma_f32_16x16x32_bf16 ----
+// A staged operand is [column][sample] bf16, column stride kBfStride (64 samples + 8 pad:
+// 144 B, so the 16 columns one ds_read_b128 group reads start on distinct banks).  The
+// MFMA reader, lane l = (g = l>>4, c = l&15), finds samples 32m + 8g .. +7 of column c
+// contiguous: one ds_read_b128 per K-step.  The writer (lane = sample) stores one bf16
+// per column; values are already bf16-rounded (Stage::rnd), so the conversion is the
+// top half of the float.  A tile over a wave's 64 samples is TWO K = 32 steps (the f32
+// path needs 16 K = 4 steps, 32 cycles each: the bf16 instance's dW costs 1/16 of it).
+constexpr int kBfStride = 72;
+static_assert(16 * kBfStride / 2 <= kStgArr, "a bf16 staged operand fits the f32 staging array");
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int N>
+DTP_DEV void stage_cols_bf(float* __restrict__ buf, int lane, int c0, const float (&v)[16]) {
+  unsigned short* p = reinterpret_cast<unsigned short*>(buf) + c0 * kBfStride + lane;
+#pragma unroll
+  for (int c = 0; c < N; ++c) p[c * kBfStride] = (unsigned short)(__float_as_uint(v[c]) >> 16);
+}
+
+DTP_DEV void stage_one_bf(float* __restrict__ buf, int lane, int col, float v) {
+  reinterpret_cast<unsigned short*>(buf)[col * kBfStride + lane] = (unsigned short)(__float_as_uint(v) >> 16);
+}
+
+struct TileOpsBf {
+  u32x4_t a[2], b[2];
+};
+DTP_DEV TileOpsBf tile_ops_bf(const float* __restrict__ dzb, const float* __restrict__ hb, int lane) {
+  const int off = (lane & 15) * kBfStride + 8 * (lane >> 4);
+  const unsigned short* pa = reinterpret_cast<const unsigned short*>(dzb) + off;
+  const unsigned short* pb = reinterpret_cast<const unsigned short*>(hb) + off;
+  TileOpsBf t;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    t.a[m] = *reinterpret_cast<const u32x4_t*>(pa + 32 * m);
+    t.b[m] = *reinterpret_cast<const u32x4_t*>(pb + 32 * m);
+  }
+  return t;
+}
+template <int K>
+DTP_DEV void tile_kstep(const TileOpsBf& t, f32x4& acc0, f32x4& acc1) {
+  const bf16x8_t a = __builtin_bit_cast(bf16x8_t, t.a[K]), b = __builtin_bit_cast(bf16x8_t, t.b[K]);
+  if constexpr (K & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc1, 0, 0, 0);
+  else acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc0, 0, 0, 0);
+}
+DTP_DEV f32x4 wave_outer_acc_bf(const float* __restrict__ dzb, const float* __restrict__ hb, f32x4 acc0, int lane) {
+  const TileOpsBf t = tile_ops_bf(dzb, hb, lane);
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+  tile_kstep<0>(t, acc0, acc1);
+  tile_kstep<1>(t, acc0, acc1);
+  return acc0 + acc1;
+}
+
+// the staging / tile-operand flavour of a stage type: f32 (16 K-steps) or bf16 (2)
+template <class S>
+struct TileKind {
+  using Ops = std::conditional_t<S::BF, TileOpsBf, TileOps>;
+  static constexpr int NK = S::BF ? 2 : 16;
+  template <int N>
+  static DTP_DEV void cols(float* buf, int lane, int c0, const float (&v)[16]) {
+    if constexpr (S::BF) stage_cols_bf<N>(buf, lane, c0, v);
+    else stage_cols<N>(buf, lane, c0, v);
+  }
+  static DTP_DEV void one(float* buf, int lane, int col, float v) {
+    if constexpr (S::BF) stage_one_bf(buf, lane, col, v);
+    else stage_one(buf, lane, col, v);
+  }
+  static DTP_DEV Ops ops(const float* dzb, const float* hb, int lane) {
+    if constexpr (S::BF) return tile_ops_bf(dzb, hb, lane);
+    else return tile_ops(dzb, hb, lane);
+  }
+  static DTP_DEV f32x4 outer(const float* dzb, const float* hb, f32x4 acc, int lane) {
+    if constexpr (S::BF) return wave_outer_acc_bf(dzb, hb, acc, lane);
+    else return wave_outer_acc(dzb, hb, acc, lane);
+  }
+};
 
 }  // namespace dtp

@@ -45,6 +45,7 @@ struct TrainSmem {
   float stage[kWaves][2][2 * kStgArr];
   float data[kDataCache];
   float sink[4];  // target of the optimizer's predicated-off stores (slots past P)
+  float lossw[kBlock / kWave];  // bf16 instances: per-wave batch-loss sums (not through a bf16 tile)
 };
 
 // One lane's sample of a step: input, target (class index for CE) and validity.
@@ -125,7 +126,38 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     mr[k] = (kUpdate && own) ? a.opt_m[(size_t)model * P + p] : 0.f;
     vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
   }
-  const int t0 = a.step[model];
+  // the step number: from the host when it knows it (the persistent engine), so the
+  // first dataset indices can be requested without waiting for the counter's load
+  const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
+  // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
+  const bool explicit_idx = !FAST && smp.mode == SAMPLER_EXPLICIT;
+  int epoch = explicit_idx ? 0 : t0 / smp.steps_per_epoch;
+  int bi = explicit_idx ? 0 : t0 - epoch * smp.steps_per_epoch;
+  // FAST: this lane's dataset index of the step at (ep_, b_): the padded-list position
+  // (padding repeats from the start), looked up in the epoch's slot of the ring; -1
+  // past the batch.  The load is issued a step ahead of its use (fidx below).
+  auto fast_index = [&](int ep_, int b_) -> int {
+    const int start = b_ * smp.batch;
+    const int size = min(smp.batch, smp.num_samples - start);
+    int q = smp.rank + (start + tid) * smp.world;
+    q = q >= smp.n ? q - smp.n : q;
+    q = q < smp.n ? q : smp.n - 1;  // lanes past the batch: any in-range position
+    const int di = table_epoch(smp, ep_)[q];
+    return tid < size ? di : -1;
+  };
+  auto roll = [&](int& ep_, int& b_) {  // advance a (epoch, batch) cursor by one step, branch-free
+    const bool r_ = ++b_ == smp.steps_per_epoch;
+    b_ = r_ ? 0 : b_;
+    ep_ += r_ ? 1 : 0;
+  };
+  // FAST: the first step's indices and the second step's (in flight across the
+  // prologue), and the cursor of the step after the next one to gather
+  int e2 = epoch, b2 = bi, fidx0 = 0, fidx = 0;
+  if constexpr (FAST) {
+    fidx0 = fast_index(epoch, bi);
+    roll(e2, b2);
+    fidx = fast_index(e2, b2);
+  }
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
   for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   if (cached) {
@@ -144,10 +176,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       if (pb[k] >= 0) sm.wb[pb[k]] = wv;
     }
   }
-  // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
-  const bool explicit_idx = !FAST && smp.mode == SAMPLER_EXPLICIT;
-  int epoch = explicit_idx ? 0 : t0 / smp.steps_per_epoch;
-  int bi = explicit_idx ? 0 : t0 - epoch * smp.steps_per_epoch;
   int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
   uint32_t keys[4];
   epoch_keys(smp, epoch, keys);
@@ -180,18 +208,6 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     bp_.size = explicit_idx ? smp.batch : min(smp.batch, smp.num_samples - bp_.start);
     return bp_;
   };
-  // FAST: this lane's dataset index of the step at (ep_, b_): the padded-list position
-  // (padding repeats from the start), looked up in the epoch's slot of the ring; -1
-  // past the batch.  The load is issued a step ahead of its use (fidx below).
-  auto fast_index = [&](int ep_, int b_) -> int {
-    const int start = b_ * smp.batch;
-    const int size = min(smp.batch, smp.num_samples - start);
-    int q = smp.rank + (start + tid) * smp.world;
-    q = q >= smp.n ? q - smp.n : q;
-    q = q < smp.n ? q : smp.n - 1;  // lanes past the batch: any in-range position
-    const int di = table_epoch(smp, ep_)[q];
-    return tid < size ? di : -1;
-  };
   auto fast_gather = [&](int di) {
     SampleRegs<S> r;
     r.valid = di >= 0;
@@ -208,19 +224,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     });
     return r;
   };
-  auto roll = [&](int& ep_, int& b_) {  // advance a (epoch, batch) cursor by one step, branch-free
-    const bool r_ = ++b_ == smp.steps_per_epoch;
-    b_ = r_ ? 0 : b_;
-    ep_ += r_ ? 1 : 0;
-  };
-  // FAST: the cursor and in-flight index of the step AFTER the next one to gather
-  int e2 = epoch, b2 = bi, fidx = 0;
   SampleRegs<S> nxt;
   if constexpr (FAST) {
-    const int fidx0 = fast_index(epoch, bi);
-    roll(e2, b2);
-    fidx = fast_index(e2, b2);
-    nxt = fast_gather(fidx0);  // waits for the first index (prologue only)
+    nxt = fast_gather(fidx0);  // the first step's samples (the index loads overlapped the prologue)
   } else {
     nxt = gather(0, batch_at(epoch, bi), keys, tid, batch_at(epoch, bi).size);
   }
@@ -248,6 +254,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     f32x4 acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lacc = 0.f;  // this lane's loss over the step's chunks (bf16 instances)
 
     // FAST: batch <= kBlock, one chunk (the loop folds away: fwd, loss and bwd are
     // one straight-line region)
@@ -298,6 +305,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
         });
       }
       if (c0 == 0) DTP_STAMP(2);
+      lacc += lpart;
 
       // ---------------- backward: dX chain (VALU, LDS weight blocks) + dW tiles (MFMA, K = samples)
       if constexpr (kPipe) {
@@ -342,6 +350,10 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       }
       }
     }
+    if constexpr (S::BF) {
+      const float wl = wave_sum(lacc);
+      if (lane == 0) sm.lossw[wave] = wl;
+    }
     DTP_STAMP(8 + wave);
     DTP_STAMP(3);
     // each wave parks its partial dW tiles in its OWN staging area (no other wave
@@ -374,7 +386,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     float lsum = 0.f;
 #pragma unroll
     for (int ww = 0; ww < kWaves; ++ww)
-      lsum += sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+      lsum += S::BF ? sm.lossw[ww] : sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
     const float mean_loss = lsum * inv;
     DTP_STAMP(5);
 
@@ -656,13 +668,15 @@ void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int 
   return e;
 }
 
-// n_steps iterations in ONE persistent launch on `stream`
-int dtp_train_engine_run(void* h, int n_steps, void* stream) {
+// n_steps iterations in ONE persistent launch on `stream`, starting at step t0 (the
+// host's mirror of the device step counters; -1: read them on the device)
+int dtp_train_engine_run(void* h, int n_steps, int t0, void* stream) {
   auto* e = static_cast<TrainEngine*>(h);
   if (!e) return set_err(-1, "null engine");
   if (n_steps <= 0) return set_err(-1, "n_steps must be positive");
   if (e->mode == DTP_MODE_GRAD && n_steps != 1) return set_err(-4, "MODE_GRAD requires n_steps == 1");
   e->a.n_steps = n_steps;
+  e->a.host_t0 = t0;
   e->fn(e->a, (hipStream_t)stream);
   return check_launch("mlp_train_kernel");
 }

@@ -260,7 +260,7 @@ class FusedTrainer:
             nat.ptr(xg.epoch) if xg else None, nat.ptr(getattr(self, "wsp", None)),
             self.loss_log.shape[0], self.n_models, n_steps,
             nat.LOSS_CE if self.cfg.loss == "ce" else nat.LOSS_MSE,
-            int(self.cfg.cache_data), self.cfg.xgmi_timeout_us, int(self.cfg.precision == "bf16"), 0, smp,
+            int(self.cfg.cache_data), self.cfg.xgmi_timeout_us, int(self.cfg.precision == "bf16"), -1, smp,
             # xGMI modes sum the W gradients in-kernel -> DDP averaging 1/W there;
             # MODE_GRAD writes local means (the flat optimizer applies 1/W)
             self._hyper(1.0 / self.world if mode in (nat.MODE_XGMI_ADAM, nat.MODE_XGMI_SGD) else 1.0))
@@ -330,7 +330,9 @@ class FusedTrainer:
                 nat.check(-1, "dtp_train_engine_create")
             self._engine = e
             self._engine_run = lib.dtp_train_engine_run
-        nat.check(self._engine_run(e, k, nat.raw_stream(self._dev_index)), "dtp_train_engine_run")
+        # the host's step mirror (== the device counters) lets the kernel request its
+        # first dataset indices without waiting for the counter load
+        nat.check(self._engine_run(e, k, self.t, nat.raw_stream(self._dev_index)), "dtp_train_engine_run")
 
     def _launch(self, k: int, idx: torch.Tensor | None = None, batch_override: int | None = None):
         lib = nat.load()
