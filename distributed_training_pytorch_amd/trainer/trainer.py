@@ -61,7 +61,10 @@ class CSVLogger:
             self._w = csv.DictWriter(self._f, fieldnames=list(row.keys()), extrasaction="ignore")
             self._w.writeheader()
         self._w.writerow(row)
-        self._f.flush()
+
+    def flush(self):
+        if self.dir is not None:
+            self._f.flush()
 
     def close(self):
         if self.dir is not None:
@@ -87,8 +90,75 @@ class _DeviceBatches:
         idx = torch_distributed_indices(g.n, g.world, g.rank, self.epoch, g.seed, g.shuffle)
         idx_t = torch.tensor(idx, device=self.X.device)
         for b in range(len(self)):
-            sel = idx_t[b * g.batch:(b + 1) * g.batch]
-            yield self.X[sel], self.Y[sel]
+            yield _DevBatch(self.X, self.Y, idx_t[b * g.batch:(b + 1) * g.batch])
+
+
+class _DevBatch:
+    """One batch of ``_DeviceBatches``: the sample indices, gathered on demand.  A
+    replayed step gathers inside its graph (``index_select`` into the static batch
+    buffers), so a batch costs one small index copy on the host side."""
+
+    __slots__ = ("X", "Y", "sel")
+
+    def __init__(self, X, Y, sel):
+        self.X, self.Y, self.sel = X, Y, sel
+
+    def materialize(self):
+        return [self.X[self.sel], self.Y[self.sel]]
+
+    def gather_into(self, idx, out):
+        torch.index_select(self.X, 0, idx, out=out[0])
+        torch.index_select(self.Y, 0, idx, out=out[1])
+
+
+class _MetricRing:
+    """Logged metrics of many steps, reduced and written in one go.
+
+    PL logs (``self.log``) every ``log_every_n_steps`` batches -- every batch in the
+    reference (``log_every_n_steps=0.03125``).  Reducing and printing each of those on
+    the host costs a collective and a device->host sync per batch, which would stall
+    the replayed step after every batch.  Instead each logged step's values are stacked
+    into a device row (the graph outputs are copied before the next replay overwrites
+    them), and every ``rows`` logged steps -- and before a checkpoint and at the end of
+    ``fit`` -- the block is averaged over ranks with ONE all-reduce, copied to the host
+    once and written to ``metrics.csv`` row by row.  ``callback_metrics`` is the last
+    row of the newest block, so it trails the live step by less than ``rows`` logged
+    steps during training and is exact after ``fit``."""
+
+    def __init__(self, trainer, logger, rows: int = 64):
+        self.tr = trainer
+        self.logger = logger
+        self.rows = rows
+        self.buf = None
+        self.keys: list = []
+        self.steps: list = []
+
+    def push(self, step: int, logged: dict) -> None:
+        keys = list(logged.keys())
+        if not keys:
+            return
+        if self.buf is None or keys != self.keys:
+            self.flush()
+            self.keys = keys
+            self.buf = torch.empty(self.rows, len(keys), dtype=torch.float32, device=self.tr.device)
+        torch.stack([v.detach().float().reshape(()) for v in logged.values()], out=self.buf[len(self.steps)])
+        self.steps.append(step)
+        if len(self.steps) == self.rows:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.steps:
+            return
+        block = self.buf[:len(self.steps)]
+        if self.tr.world_size > 1:
+            comm_util.all_reduce_(block)
+            block /= self.tr.world_size
+        rows = block.tolist()
+        for step, vals in zip(self.steps, rows):
+            self.logger.log(step, dict(zip(self.keys, vals)))
+        self.logger.flush()
+        self.tr.callback_metrics = dict(zip(self.keys, rows[-1]))
+        self.steps = []
 
 
 class Trainer:
@@ -196,6 +266,7 @@ class Trainer:
         logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
         self._log_dir = logger.dir
+        metrics = _MetricRing(self, logger)
         pbar = None
         if self.enable_progress_bar and self.global_rank == 0:
             try:
@@ -217,15 +288,25 @@ class Trainer:
                 for batch_idx, batch in enumerate(loader):
                     if batch_idx < self._skip_batches:  # resumed mid-epoch: these already ran
                         continue
-                    batch = [b.to(self.device, non_blocking=True) for b in batch]
+                    dev = batch if isinstance(batch, _DevBatch) else None
+                    if dev is not None and stepper is None:
+                        batch = dev.materialize()
+                    elif dev is None:
+                        batch = [b.to(self.device, non_blocking=True) for b in batch]
                     if self._refresh_flat_opts() and stepper is not None:
                         stepper.reset()  # the captured optimizer launches hold the old hyperparameters
-                    if stepper is not None and self._static_ok(static, batch):
-                        key = tuple(tuple(b.shape) for b in batch)
-                        if key not in static:
-                            static[key] = [b.clone() for b in batch]
-                        for dst, src in zip(static[key], batch):
-                            dst.copy_(src)
+                    if stepper is not None and (dev is not None or self._static_ok(static, batch)):
+                        if dev is not None:  # indices in, gather inside the replayed step
+                            key = ("idx", dev.sel.shape[0])
+                            if key not in static:
+                                static[key] = _StaticBatch(dev.materialize(), dev.sel.clone(), dev)
+                            static[key].idx.copy_(dev.sel)
+                        else:
+                            key = tuple(tuple(b.shape) for b in batch)
+                            if key not in static:
+                                static[key] = _StaticBatch([b.clone() for b in batch])
+                            for dst, src in zip(static[key].tensors, batch):
+                                dst.copy_(src)
                         self._cur_batch_idx = batch_idx  # read by the body only while capturing
                         replay = stepper.is_captured(key)
                         stepper.run(key)
@@ -239,15 +320,11 @@ class Trainer:
                     self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
                     self._batch_in_epoch = batch_idx + 1
                     if self.global_step % self.log_every_n_steps == 0:
-                        metrics = {k: v for k, v in model._logged.items()}
-                        vals = torch.stack([v.float().reshape(()) for v in metrics.values()]).to(self.device)
-                        comm_util.all_reduce_(vals)
-                        vals /= self.world_size
-                        self.callback_metrics = dict(zip(metrics.keys(), vals.tolist()))
-                        logger.log(self.global_step, self.callback_metrics)
+                        metrics.push(self.global_step, model._logged)
                     if pbar is not None:
                         pbar.update(1)
                     if self.every_n_train_steps and self.global_step % self.every_n_train_steps == 0:
+                        metrics.flush()
                         self._save(model, opts, "last.ckpt")
                     if 0 < self.max_steps <= self.global_step:
                         done = True
@@ -258,6 +335,7 @@ class Trainer:
                 self._skip_batches = 0
                 if self.max_epochs is not None and self.current_epoch >= self.max_epochs:
                     done = True
+            metrics.flush()
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             self.fit_time = time.perf_counter() - t0
@@ -408,7 +486,10 @@ class Trainer:
         static: dict = {}
 
         def body(key):
-            self._optimizer_steps(model, ddp, opts, static[key], self._cur_batch_idx)
+            sb = static[key]
+            if sb.idx is not None:
+                sb.src.gather_into(sb.idx, sb.tensors)
+            self._optimizer_steps(model, ddp, opts, sb.tensors, self._cur_batch_idx)
 
         def abort():
             if getattr(model, "_toggled", None):
@@ -424,6 +505,16 @@ class Trainer:
         if dist.is_initialized():
             comm_util.barrier()
             dist.destroy_process_group()
+
+
+class _StaticBatch:
+    """The batch buffers a captured step reads (and, for device batches, the index
+    buffer it gathers them with)."""
+
+    __slots__ = ("tensors", "idx", "src")
+
+    def __init__(self, tensors, idx=None, src=None):
+        self.tensors, self.idx, self.src = tensors, idx, src
 
 
 def _cpu_state(x):

@@ -189,3 +189,19 @@ def test_post_accumulate_hooks_fire_for_none_grads_and_flatddp_counts_once():
     x = torch.ones(3, requires_grad=True)
     (F.apply(x, ws[0]).sum() + F.apply(x, ws[1]).sum()).backward()
     assert reduced and reduced[0][1] == 2, reduced  # released only once both parameters reported
+
+
+def test_trainer_metric_rows_cover_every_logged_step(tmp_path):
+    """Logged metrics are reduced and written in blocks (one sync per 64 logged
+    steps), but metrics.csv still holds one row per logged step with that step's
+    values, and callback_metrics is the last step's after fit."""
+    import csv
+
+    steps = 70
+    tr, _ = _lit_run(tmp_path, steps)
+    rows = list(csv.DictReader(open(tmp_path / "lightning_logs" / "version_0" / "metrics.csv")))
+    assert [int(r["step"]) for r in rows] == list(range(1, steps + 1))
+    keys = [k for k in rows[0] if k != "step"]
+    assert keys and set(keys) == set(tr.callback_metrics)
+    assert all(float(rows[-1][k]) == tr.callback_metrics[k] for k in keys)
+    assert len({rows[i][keys[0]] for i in range(steps)}) > steps // 2  # per-step values, not one repeated
