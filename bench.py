@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32 = the reference's precision=32 (the headline); bf16 = bf16 matmul operands, "
                          "fp32 accumulation / master weights / Adam (BASELINE config 2)")
+    ap.add_argument("--cu-mask", choices=["off", "on"], default="off",
+                    help="on: run the train kernel on a stream pinned to the first n_models CUs, so its "
+                         "code stays in those CUs' instruction cache between launches")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:(local_rank %% device_count), gloo process group "
@@ -110,6 +113,10 @@ def main():
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         cfg_desc = {"launch": "eager", "comm": "rccl DDP + gloo loss reduce" if world > 1 else "none"}
     else:
+        if a.cu_mask == "on" and dev.type == "cuda":
+            from distributed_training_pytorch_amd import _native
+
+            torch.cuda.set_stream(_native.cu_masked_stream(dev, [0, 1]))
         X, Y = ds.device_tensors(dev)
         geom = SamplerGeometry(n=n, world=world, rank=rank, batch=a.batch, seed=a.seed)
         torch.manual_seed(a.seed)
@@ -123,7 +130,7 @@ def main():
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm,
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
-                    else "Feistel shuffle"}
+                    else "Feistel shuffle", "cu_mask": a.cu_mask}
 
     # the timed region is bracketed by an all-rank barrier + synchronize on both sides;
     # ranks of the in-kernel xGMI engine use the framework's device barrier (one xGMI

@@ -247,6 +247,8 @@ def _declare(lib):
         "dtp_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
         "dtp_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
         "dtp_stream_sync": (c_int, [c_void_p]),
+        "dtp_stream_create_cu_mask": (c_int, [ctypes.POINTER(ctypes.c_uint), c_int, ctypes.POINTER(c_void_p)]),
+        "dtp_stream_destroy": (c_int, [c_void_p]),
         "dtp_device_sync_check": (c_int, []),
         "dtp_graph_capture_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                             P(c_void_p)]),
@@ -398,3 +400,19 @@ def set_wait_mode(mode: str | None = None) -> str:
 def native_enabled() -> bool:
     """DTP_NATIVE=0 forces the PyTorch reference path (debug only; never on a timed run)."""
     return os.environ.get("DTP_NATIVE", "1") != "0"
+
+
+def cu_masked_stream(device, cus) -> "torch.cuda.ExternalStream":
+    """A torch stream whose kernels run only on the listed logical CUs
+    (``hipExtStreamCreateWithCUMask``); it lives for the rest of the process."""
+    lib = require(torch.device(device))
+    cus = sorted(set(int(c) for c in cus))
+    if not cus or cus[0] < 0:
+        raise ValueError(f"cu_masked_stream: bad CU list {cus}")
+    words = cus[-1] // 32 + 1
+    mask = (ctypes.c_uint * words)()
+    for c in cus:
+        mask[c // 32] |= 1 << (c % 32)
+    out = ctypes.c_void_p()
+    check(lib.dtp_stream_create_cu_mask(mask, words, ctypes.byref(out)), "dtp_stream_create_cu_mask")
+    return torch.cuda.ExternalStream(out.value, device=torch.device(device))

@@ -105,6 +105,19 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
+  // PROF: kernel entry and exit stamps of the launch (slots 20 and 21 of iteration 0)
+  auto stamp_launch = [&](int slot) {
+    if constexpr (PROF) {
+      if (tid == 0) {
+        unsigned long long t_;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        prof[(size_t)blockIdx.x * 8 * 32 + slot] = t_;
+      }
+    }
+  };
+  stamp_launch(20);
   const bool ce = !FAST && a.loss == DTP_LOSS_CE;  // FAST: MSE
   const int ydim = ce ? 1 : S::OUT;
   const float slope = a.hp.slope;
@@ -477,6 +490,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     }
     if (tid == 0) a.step[model] = t0 + a.n_steps;
     if (kXgmi && tid == 0) a.epoch[model] = xepoch;
+    stamp_launch(21);
   }
 }
 

@@ -146,6 +146,25 @@ int dtp_stream_sync(void* stream) {
   return 0;
 }
 
+// A stream whose kernels run only on the CUs set in `mask` (`words` 32-bit words,
+// bit i = logical CU i).  The persistent train kernel is one workgroup per model:
+// pinning its launches to the same few CUs keeps its code in those CUs' instruction
+// cache from one launch to the next, instead of refetching it on whichever CUs the
+// dispatcher picks (bench.py --cu-mask).
+int dtp_stream_create_cu_mask(const unsigned* mask, int words, void** out) {
+  *out = nullptr;
+  if (!mask || words <= 0) return -1;
+  hipStream_t s = nullptr;
+  RT_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
+  *out = s;
+  return 0;
+}
+
+int dtp_stream_destroy(void* stream) {
+  if (stream) RT_CHECK(hipStreamDestroy((hipStream_t)stream));
+  return 0;
+}
+
 // debug mode (DTP_DEBUG=1): drain the device after a native call and surface any
 // asynchronous kernel fault at the call that caused it
 int dtp_device_sync_check(void) {

@@ -52,6 +52,12 @@ def main():
             d["bwd_layers(top->0)"] = [int(b - a) for a, b in zip([int(s[2])] + bl[:-1], bl)]
             rows.append(d)
         res[rep] = rows[-1]
+        # the launch's first step (cold instruction cache, LDS state just loaded)
+        res[rep]["first_step_total"] = int(st[0, 0, 7] - st[0, 0, 0])
+        # kernel entry -> first step start (parameter / dataset loads, weight scatter,
+        # Adam table), and last step end -> write-back issued
+        res[rep]["prologue"] = int(st[0, 0, 0] - st[0, 0, 20])
+        res[rep]["epilogue"] = int(st[0, 0, 21] - st[0, 7, 7])
     print(json.dumps(res, indent=1))
     # also the wall time per step of the plain persistent kernel
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
