@@ -3,6 +3,7 @@ scalar Feistel reference, BatchIndexer hands out the same batches as the host
 lists (device sampler and exact DistributedSampler order), and LossRing reduces a
 chunk of per-step losses to the same global means as a per-step all-reduce."""
 import torch
+import pytest
 
 from distributed_training_pytorch_amd.data import sampler as S
 
@@ -97,3 +98,19 @@ def test_permutation_ring_cpu_refill_and_order():
             assert [perm[q] for q in pos] == ref, e
     if ring._thread is not None:
         ring._thread.join()
+
+
+def test_library_build_stamp_ties_the_kernels_to_the_sources(monkeypatch):
+    """libdtp.so carries the hash of the csrc tree and flags it was built from
+    (``dtp_source_hash``); loading it next to different sources fails loudly instead of
+    running stale kernels."""
+    from distributed_training_pytorch_amd import _native as nat
+    from distributed_training_pytorch_amd import build
+
+    lib = nat.load()
+    assert nat.source_hash() == build.source_hash() and len(build.source_hash()) >= 16
+    monkeypatch.delenv("DTP_SKIP_STAMP", raising=False)
+    monkeypatch.delenv("DTP_LIB", raising=False)
+    monkeypatch.setattr(build, "source_hash", lambda: "f" * 64)
+    with pytest.raises(nat.NativeUnavailable, match="stale"):
+        nat.check_stamp(lib)
