@@ -527,6 +527,15 @@ def _cpu_state(x):
     return x
 
 
+_GROUP_KEYS = ("lr", "betas", "eps", "weight_decay", "momentum", "dampening", "nesterov", "amsgrad", "maximize",
+               "differentiable", "decoupled_weight_decay")
+
+
+def _group_key(opt):
+    g = opt.param_groups[0]
+    return (type(opt), len(opt.param_groups)) + tuple(g.get(k) for k in _GROUP_KEYS)
+
+
 def _optim_config(opt):
     """OptimConfig of a plain Adam/SGD's single param group, or None if the flat kernel
     cannot run it (several groups, tensor lr, amsgrad, nesterov, ...)."""
@@ -567,6 +576,7 @@ class _FlatTorchOptimizer:
         self.params = params
         self.cfg = cfg
         self.flat = FlatOptimizer(flat_p, flat_g, cfg)
+        self._key = _group_key(opt)
         self._import_state()
 
     def _import_state(self):
@@ -593,7 +603,12 @@ class _FlatTorchOptimizer:
 
     def refresh(self):
         """True if the param group's hyperparameters changed (now applied), False if
-        not, None if the optimizer no longer fits the flat kernel."""
+        not, None if the optimizer no longer fits the flat kernel.  Called every batch:
+        an unchanged param group is recognised from a tuple of its entries."""
+        key = _group_key(self.opt)
+        if key == self._key:
+            return False
+        self._key = key
         cfg = _optim_config(self.opt)
         if cfg is None or cfg.name != self.cfg.name:
             return None

@@ -10,4 +10,6 @@ bash scripts/gpu_steps.sh \
   "120|r3g/demo_torch|python demo.py --iters 1000 --seed 0 --no_progress" \
   "120|r3g/demo_device|python demo.py --iters 1000 --seed 0 --no_progress --sampler device" \
   "180|r3g/lt_prof|python -m cProfile -o gpurun_out/r3g/lt.prof demo_pytorch_lightning.py --gpus 1 --steps 1000 --no_progress --root_dir /tmp/lt" \
-  "60|r3g/lt_stats|python -c \"import pstats; pstats.Stats('gpurun_out/r3g/lt.prof').sort_stats('tottime').print_stats(30)\""
+  "60|r3g/lt_stats|python -c \"import pstats; pstats.Stats('gpurun_out/r3g/lt.prof').sort_stats('tottime').print_stats(30)\"" \
+  "120|r3g/demo_prof|python -m cProfile -o gpurun_out/r3g/demo.prof demo.py --iters 1000 --seed 0 --no_progress" \
+  "60|r3g/demo_stats|python -c \"import pstats; pstats.Stats('gpurun_out/r3g/demo.prof').sort_stats('tottime').print_stats(30)\""

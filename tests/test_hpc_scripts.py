@@ -185,3 +185,31 @@ def test_scripts_are_valid_bash():
     for p in list(HPC.rglob("*.sh")) + list((ROOT / "interactive_job_cmds").glob("*.sh")) + [HPC / "count_sweeps.bash"]:
         r = subprocess.run(["bash", "-n", str(p)], capture_output=True, text=True)
         assert r.returncode == 0, (p, r.stderr)
+
+
+def test_singularity_job_builds_the_container_command(fakeenv, tmp_path):
+    """The Singularity/Apptainer job: the container is staged to the node's
+    temp dir and run with --rocm (not --nv), the results / data / tmp / source bind
+    mounts, the experiment command, and the RCCL/IPC environment passed inside."""
+    env, log, scratch = fakeenv
+    fake = tmp_path / "bin" / "apptainer"
+    fake.write_text('#!/bin/bash\necho "apptainer $* | ipc=$SINGULARITYENV_HSA_ENABLE_IPC_MODE_LEGACY '
+                    'procid=$SINGULARITYENV_SLURM_PROCID" >> "$FAKE_LOG"\n')
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    rs = tmp_path / "bin" / "rsync"  # rsync may be missing on the test host: copy the last two args
+    rs.write_text('#!/bin/bash\ncp "${@: -2:1}" "${@: -1}"\n')
+    rs.chmod(rs.stat().st_mode | stat.S_IEXEC)
+    image = tmp_path / "dtp_rocm.sif"
+    image.write_text("image")
+    node_tmp = tmp_path / "node"
+    e = dict(env, source_dir=str(ROOT), scratch_dir=str(scratch), exp_name="exp1", singularity_container=str(image),
+             SLURM_TMPDIR=str(node_tmp), SLURM_JOB_ID="42", SLURM_PROCID="3",
+             cmd="python demo.py --iters 3 --backend=nccl")
+    run(["bash", str(HPC / "singularity_hpc_files" / "standard_job.sh"), "", "code"], e)
+    line = [l for l in log.read_text().splitlines() if l.startswith("apptainer ")][-1]
+    assert line.startswith("apptainer run --rocm ") and "--nv" not in line
+    assert f"-B {scratch}/exp1:/results" in line and f"-B {node_tmp}/data:/data" in line
+    assert f"-B {ROOT}:/code --pwd /code" in line
+    assert f"{node_tmp}/dtp_rocm.sif python demo.py --iters 3 --backend=nccl" in line
+    assert line.endswith("ipc=0 procid=3")
+    assert (node_tmp / "dtp_rocm.sif").exists() and (scratch / "exp1").is_dir()
