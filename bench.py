@@ -152,8 +152,17 @@ def main():
             sync()
             comm_util.barrier()
 
-    # warmup (untimed)
-    train(a.warmup)
+    # warmup (untimed): the W steps, spread over up to 16 launches.  The first few
+    # launches of a process pay extra runtime latency; with W = 5 in ONE launch the
+    # timed call was only the process's second launch (K = 20, 8 fresh processes each,
+    # interleaved: 5.96 vs 5.52 us/step median, profiles/r3_gpu/k20_warmup_launches.jsonl).
+    # DTP_BENCH_WARMUP_LAUNCHES overrides the count.
+    split = max(1, min(a.warmup, int(os.environ.get("DTP_BENCH_WARMUP_LAUNCHES", "16"))))
+    done = 0
+    for i in range(split):
+        k = (a.warmup - done) // (split - i)
+        train(k)
+        done += k
     sync_barrier()
     sync()
     t0 = time.perf_counter()

@@ -100,8 +100,11 @@ def main(argv=None):
         sps = None
         if getattr(trainer, "fit_time", None):
             sps = trainer.global_step * a.batch_size * getattr(trainer, "world_size", 1) / trainer.fit_time
+        steady = None  # after the first 10 batches (eager warm-up, graph capture, first kernel loads)
+        if getattr(trainer, "steady_time", None):
+            steady = trainer.steady_steps * a.batch_size * getattr(trainer, "world_size", 1) / trainer.steady_time
         print(f"[Process 0] summary: {{'global_step': {trainer.global_step}, 'metrics': {trainer.callback_metrics}, "
-              f"'checkpoint': {trainer.checkpoint_path!r}, 'samples_per_s': {sps}, "
+              f"'checkpoint': {trainer.checkpoint_path!r}, 'samples_per_s': {sps}, 'steady_samples_per_s': {steady}, "
               f"'graph_replays': {getattr(trainer, 'graph_replays', 0)}}}", flush=True)
     if hasattr(trainer, "teardown"):
         trainer.teardown()

@@ -177,10 +177,12 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
     for (int e = tid; e < smp.n * ydim; e += kBlock) sm.data[smp.n * S::IN + e] = a.Y[e];
   }
+  stamp_launch(18);
   const float* __restrict__ Xg = a.X;
   const float* __restrict__ Yg = a.Y;
   const int yoff = smp.n * S::IN;
   __syncthreads();  // weight blocks zeroed (pads stay 0) before the owners scatter into them
+  stamp_launch(19);
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     if (NPT * tid + k < P) {
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       if (pb[k] >= 0) sm.wb[pb[k]] = wv;
     }
   }
+  stamp_launch(22);
   int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
   uint32_t keys[4];
   epoch_keys(smp, epoch, keys);
@@ -254,8 +257,10 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     }
   };
   if (kAdam) fill_adam(0);
+  stamp_launch(23);
   float* const stg_pack = &sm.stage[wave][0][0];
   __syncthreads();  // scattered weight blocks and the Adam table visible to every wave
+  stamp_launch(29);
 
   for (int it = 0; it < a.n_steps; ++it) {
     DTP_STAMP(0);

@@ -111,6 +111,9 @@ class _DevBatch:
         torch.index_select(self.Y, 0, idx, out=out[1])
 
 
+_STEADY_AFTER = 10  # batches excluded from Trainer.steady_time
+
+
 class _MetricRing:
     """Logged metrics of many steps, reduced and written in one go.
 
@@ -278,6 +281,9 @@ class Trainer:
                 pbar = None
         model.on_train_start()
         t0 = time.perf_counter()
+        # steady-state clock: from the end of batch _STEADY_AFTER on (warm-up batches,
+        # graph capture and first kernel loads excluded); synchronised at both ends
+        self.steady_time, self.steady_steps, steady_t0, steady_from = None, 0, None, self.global_step + _STEADY_AFTER
         done = 0 < self.max_steps <= self.global_step
         try:
             while not done:
@@ -318,6 +324,10 @@ class Trainer:
                     else:
                         self._optimizer_steps(model, ddp, opts, batch, batch_idx)
                     self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
+                    if self.global_step == steady_from:
+                        if self.device.type == "cuda":
+                            torch.cuda.synchronize(self.device)
+                        steady_t0 = time.perf_counter()
                     self._batch_in_epoch = batch_idx + 1
                     if self.global_step % self.log_every_n_steps == 0:
                         metrics.push(self.global_step, model._logged)
@@ -339,6 +349,9 @@ class Trainer:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             self.fit_time = time.perf_counter() - t0
+            if steady_t0 is not None and self.global_step > steady_from:
+                self.steady_time = time.perf_counter() - steady_t0
+                self.steady_steps = self.global_step - steady_from
             if stepper is not None:
                 self.graph_replays = stepper.replays
         finally:

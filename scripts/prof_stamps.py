@@ -58,6 +58,12 @@ def main():
         # Adam table), and last step end -> write-back issued
         res[rep]["prologue"] = int(st[0, 0, 0] - st[0, 0, 20])
         res[rep]["epilogue"] = int(st[0, 0, 21] - st[0, 7, 7])
+        # prologue detail (thread 0's view): dataset copied to LDS (18), first barrier
+        # (19), weights scattered (22), Adam table filled (23), second barrier (29)
+        marks = [("entry->data_copied", 20, 18), ("->barrier1", 18, 19), ("->weights_scattered", 19, 22),
+                 ("->adam_table", 22, 23), ("->barrier2", 23, 29), ("->step0_start", 29, None)]
+        res[rep]["prologue_detail"] = {name: int((st[0, 0, b] if b is not None else st[0, 0, 0]) - st[0, 0, a])
+                                       for name, a, b in marks}
     print(json.dumps(res, indent=1))
     # also the wall time per step of the plain persistent kernel
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
