@@ -193,6 +193,9 @@ class GemmArgs(ctypes.Structure):
         ("vec_b", c_int),
         ("force_big", c_int),
         ("fast", c_int),
+        ("pad_", c_int),
+        ("work", c_void_p),
+        ("work_bytes", c_longlong),
     ]
 
 
@@ -256,6 +259,7 @@ def _declare(lib):
         "dtp_graph_destroy": (c_int, [c_void_p]),
         "dtp_struct_sizes": (c_int, [P(c_int)]),
         "dtp_gemm": (c_int, [P(GemmArgs), c_void_p]),
+        "dtp_gemm_workspace": (c_longlong, [P(GemmArgs)]),
         "dtp_xgmi_allreduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_float,
                                        c_void_p, c_int, c_void_p]),
         "dtp_xgmi_allreduce_epoch_slots": (c_int, [c_int]),

@@ -167,9 +167,14 @@ struct DtpGemmArgs {
   int vec_a, vec_b;  // set by dtp_gemm (16-byte loads allowed)
   int force_big;     // tests: take the 256x256 bf16 kernel for any layout it supports
   int fast;          // LDS-DMA 256x256 bf16 kernel: 0 auto, 1 whenever its preconditions hold, -1 never
+  int pad_;
+  void* work;              // split-K partial sums of the 8-phase kernel (splitk = 0: dtp_gemm picks)
+  long long work_bytes;
 };
 
 int dtp_gemm(const DtpGemmArgs* a, void* stream);
+// bytes of DtpGemmArgs::work the call would use with splitk = 0 (0: no split-K plan)
+long long dtp_gemm_workspace(const DtpGemmArgs* a);
 // out[n] (+)= sum_m X[m*ld+n]  (bias gradients)
 int dtp_colsum(const void* X, long long ld, int M, int N, int dtype, float* out, int accumulate, void* stream);
 

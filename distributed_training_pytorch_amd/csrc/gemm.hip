@@ -27,38 +27,18 @@
 //    L2), then grouped 8 M-tiles at a time for operand reuse in that L2.
 #include "dtp_common.h"
 #include "dtp_api.h"
+#include "gemm_epi.h"
 
 namespace dtp {
 namespace gemm {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
 constexpr int kBM = 128, kBN = 128, kThreads = 256;
 constexpr int kChunks = 8;  // 16-byte chunks per 128-byte LDS row
 
-template <int DT>
-struct Ty {
-  static constexpr int ES = DT == DTP_DT_BF16 ? 2 : 4;  // element bytes
-  static constexpr int EPC = 16 / ES;                    // elements per 16-byte chunk
-  static constexpr int BK = 128 / ES;                    // K per tile (one LDS row)
-};
 
 DTP_DEV int swz(int row) { return (row ^ (row >> 3)) & 7; }
 DTP_DEV int slot(int row, int chunk) { return row * kChunks + (chunk ^ swz(row)); }
 
-DTP_DEV float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
-DTP_DEV uint16_t f32_to_bf16(float f) {  // round to nearest even
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return uint16_t((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return uint16_t(u >> 16);
-}
-
-template <int DT>
-DTP_DEV float load_elem(const char* p) {
-  if constexpr (DT == DTP_DT_BF16) return bf16_to_f32(*reinterpret_cast<const uint16_t*>(p));
-  else return *reinterpret_cast<const float*>(p);
-}
 
 // 16 bytes of row `r` (memory row), elements [c, c+EPC) of a matrix with `rows` rows,
 // `cols` columns and leading dimension `ld`; out-of-range elements read as 0.
@@ -154,51 +134,6 @@ DTP_DEV void stage_store(const Stage<ROWS>& s, uint4* __restrict__ lds, int tid)
           *dst = make_uint2(lo, hi);
         }
       }
-    }
-  }
-}
-
-// tile decode shared by both kernels: XCD-aware remap (workgroups are dealt
-// round-robin over the 8 XCDs: consecutive tile ids land on one XCD's L2), then
-// 8-row groups of M tiles, split-K innermost
-struct TileId {
-  int m0, n0, ks;
-};
-template <int BMT, int BNT>
-DTP_DEV TileId decode_tile(const DtpGemmArgs& a) {
-  const int tm = (a.M + BMT - 1) / BMT, tn = (a.N + BNT - 1) / BNT;
-  int b = blockIdx.x;
-  const int nb = gridDim.x;
-  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
-  TileId id;
-  id.ks = b % a.splitk;
-  const int t = b / a.splitk;
-  const int group = t / (8 * tn), first_m = group * 8;
-  const int gsz = min(tm - first_m, 8);
-  id.m0 = (first_m + (t % (8 * tn)) % gsz) * BMT;
-  id.n0 = ((t % (8 * tn)) / gsz) * BNT;
-  return id;
-}
-
-// fused epilogue of one output element
-template <int DT>
-DTP_DEV void epilogue_store(const DtpGemmArgs& a, char* C, const char* aux, int m, int n, float acc, float bias) {
-  float v = a.alpha * acc + bias;
-  if (aux) v *= leaky_grad_from_out(load_elem<DT>(aux + (static_cast<long long>(m) * a.ldaux + n) * Ty<DT>::ES),
-                                    a.slope);
-  if (a.act) v = leaky(v, a.slope);
-  const long long off = static_cast<long long>(m) * a.ldc + n;
-  if (a.out_dtype == DTP_DT_BF16) {
-    uint16_t* p = reinterpret_cast<uint16_t*>(C) + off;
-    if (a.accumulate) v += bf16_to_f32(*p);
-    *p = f32_to_bf16(v);
-  } else {
-    float* p = reinterpret_cast<float*>(C) + off;
-    if (a.splitk > 1) {
-      atomicAdd(p, v);
-    } else {
-      if (a.accumulate) v += *p;
-      *p = v;
     }
   }
 }
@@ -520,130 +455,6 @@ DTP_DEV void fast_epilogue(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], int m
   }
 }
 
-// LDS-staged epilogue of the 256x256 LDS-DMA kernel (the operand images are dead
-// once the K loop ends).  The MFMA layout gives a lane one column and 4 rows per
-// fragment, so a direct store writes 2-4 bytes per lane and the aux / accumulate
-// operands come back one scalar load at a time.  Instead each wave parks its
-// 128x64 f32 sub-tile in its own LDS region, 64 rows per pass (row stride 68
-// floats: the ds_write_b32 of one fragment register hits 64 distinct banks), and
-// reads it back row-major: lane L owns 8 adjacent columns 8 (L & 7) .. +8 of rows
-// L / 8 + 8 t, so aux, the old C (accumulate) and C itself move as 16-byte vectors
-// (8 lanes = one 128-byte bf16 row segment).  Columns past N (ragged last tile) or
-// unaligned operands take the per-element path.
-constexpr int kEpiStride = 68;
-constexpr int kEpiWaveFloats = 64 * kEpiStride;
-
-DTP_DEV void bf16x8_to_f32(const uint4& g, float (&x)[8]) {
-  const uint32_t w[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    x[2 * q] = __uint_as_float(w[q] << 16);
-    x[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
-  }
-}
-
-// one pass = fragment rows 4H .. 4H+3 (H a template parameter: acc is indexed
-// statically, so it stays in registers)
-// (J0: first of the 4 fragment columns staged, for waves holding more than 4)
-template <int H, int J0 = 0, int NJ = 4>
-DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ], float* buf, const float (&bias)[8],
-                                int m0, int wr, int ncol, bool vec, int lane) {
-  const int lr = lane & 15, lg = lane >> 4, c8 = lane & 7, rl = lane >> 3;
-  char* C = static_cast<char*>(a.C);
-  const uint16_t* aux = static_cast<const uint16_t*>(a.aux);
-  const bool bf16_out = a.out_dtype == DTP_DT_BF16;
-  constexpr int h = H;
-  {
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) buf[(16 * ii + 4 * lg + r) * kEpiStride + 16 * j + lr] = acc[4 * h + ii][J0 + j][r];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's stores land before its own reads (LDS is in order per wave)
-#pragma unroll
-    for (int t0 = 0; t0 < 8; t0 += 4) {
-      float v[4][8];
-      int mrow[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int lrow = rl + 8 * (t0 + u);
-        mrow[u] = m0 + wr * 128 + 64 * h + lrow;
-        const float4 x0 = *reinterpret_cast<const float4*>(buf + lrow * kEpiStride + 8 * c8);
-        const float4 x1 = *reinterpret_cast<const float4*>(buf + lrow * kEpiStride + 8 * c8 + 4);
-        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[u][c] = xs[c];
-      }
-      if (vec) {
-        // every operand of the 4 rows requested before any is used (rows past M clamped, never stored)
-        uint4 g[4], oc[4][2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const long long mr = min(mrow[u], a.M - 1);
-          if (aux) g[u] = *reinterpret_cast<const uint4*>(aux + mr * a.ldaux + ncol);
-          if (a.accumulate) {
-            if (bf16_out) {
-              oc[u][0] = *reinterpret_cast<const uint4*>(C + (mr * a.ldc + ncol) * 2);
-            } else {
-              oc[u][0] = *reinterpret_cast<const uint4*>(C + (mr * a.ldc + ncol) * 4);
-              oc[u][1] = *reinterpret_cast<const uint4*>(C + (mr * a.ldc + ncol + 4) * 4);
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          float y[8];
-#pragma unroll
-          for (int c = 0; c < 8; ++c) y[c] = a.alpha * v[u][c] + bias[c];
-          if (aux) {
-            float gv[8];
-            bf16x8_to_f32(g[u], gv);
-#pragma unroll
-            for (int c = 0; c < 8; ++c) y[c] *= leaky_grad_from_out(gv[c], a.slope);
-          }
-          if (a.act) {
-#pragma unroll
-            for (int c = 0; c < 8; ++c) y[c] = leaky(y[c], a.slope);
-          }
-          if (mrow[u] >= a.M) continue;
-          const long long off = static_cast<long long>(mrow[u]) * a.ldc + ncol;
-          if (bf16_out) {
-            if (a.accumulate) {
-              float ov[8];
-              bf16x8_to_f32(oc[u][0], ov);
-#pragma unroll
-              for (int c = 0; c < 8; ++c) y[c] += ov[c];
-            }
-            uint32_t o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = uint32_t(f32_to_bf16(y[2 * q])) | (uint32_t(f32_to_bf16(y[2 * q + 1])) << 16);
-            *reinterpret_cast<uint4*>(C + off * 2) = make_uint4(o[0], o[1], o[2], o[3]);
-          } else {
-            if (a.accumulate) {
-              const uint32_t w[8] = {oc[u][0].x, oc[u][0].y, oc[u][0].z, oc[u][0].w,
-                                     oc[u][1].x, oc[u][1].y, oc[u][1].z, oc[u][1].w};
-#pragma unroll
-              for (int c = 0; c < 8; ++c) y[c] += __uint_as_float(w[c]);
-            }
-            *reinterpret_cast<float4*>(C + off * 4) = make_float4(y[0], y[1], y[2], y[3]);
-            *reinterpret_cast<float4*>(C + (off + 4) * 4) = make_float4(y[4], y[5], y[6], y[7]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (mrow[u] >= a.M) continue;
-#pragma unroll
-          for (int c = 0; c < 8; ++c)
-            if (ncol + c < a.N)
-              epilogue_store<DTP_DT_BF16>(a, C, static_cast<const char*>(a.aux), mrow[u], ncol + c, v[u][c], bias[c]);
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this pass done before the next pass overwrites
-  }
-}
 
 DTP_DEV void fast_epilogue_lds(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], char* lds, int m0, int n0, int wave,
                                int wr, int wc, int lane) {
@@ -654,8 +465,8 @@ DTP_DEV void fast_epilogue_lds(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], c
   float bias[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) bias[c] = (a.bias && ncol + c < a.N) ? a.bias[ncol + c] : 0.f;
-  fast_epilogue_pass<0>(a, acc, buf, bias, m0, wr, ncol, vec, lane);
-  fast_epilogue_pass<1>(a, acc, buf, bias, m0, wr, ncol, vec, lane);
+  fast_epilogue_pass<0>(a, acc, buf, bias, m0 + wr * 128, ncol, vec, lane);
+  fast_epilogue_pass<1>(a, acc, buf, bias, m0 + wr * 128 + 64, ncol, vec, lane);
 }
 
 // VAR (schedule experiments, selected by DtpGemmArgs::fast = 2 + VAR): bit 0 = static
@@ -857,8 +668,8 @@ __global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1
     float bias[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) bias[c] = (a.bias && ncol + c < a.N) ? a.bias[ncol + c] : 0.f;
-    fast_epilogue_pass<0, 4 * jh, 8>(a, acc, ebuf, bias, m0, wr, ncol, vec, lane);
-    fast_epilogue_pass<1, 4 * jh, 8>(a, acc, ebuf, bias, m0, wr, ncol, vec, lane);
+    fast_epilogue_pass<0, 4 * jh, 8>(a, acc, ebuf, bias, m0 + wr * 128, ncol, vec, lane);
+    fast_epilogue_pass<1, 4 * jh, 8>(a, acc, ebuf, bias, m0 + wr * 128 + 64, ncol, vec, lane);
   };
   half(std::integral_constant<int, 0>{});
   half(std::integral_constant<int, 1>{});
@@ -876,8 +687,8 @@ int launch_w4(const DtpGemmArgs& a, hipStream_t s) {
   return check_launch("dtp_gemm(LDS-DMA 256x256, 4 waves)");
 }
 
-constexpr int kFastDefaultVar = 2;  // next tile's DMA split over the k-steps: +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl; the ring schedules
-                                     // measured there live on branch exp/gemm-ring)
+constexpr int kFastDefaultVar = 2;  // two-buffer kernel's schedule when the 8-phase one cannot run: next tile's DMA split over the
+                                     // k-steps, +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl)
 
 template <int VAR>
 int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
@@ -1142,6 +953,25 @@ using namespace dtp;
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// the 8-phase kernel's preconditions (bf16, whole 64-deep K-tiles, 16-byte aligned rows,
+// a transposed operand in whole 8-element chunks); its per-K-tile DMA offsets are
+// 32-bit, so a transposed operand's K rows must span < 4 GiB
+static bool ph8_shape(const DtpGemmArgs& a) {
+  return a.dtype == DTP_DT_BF16 && a.K % 64 == 0 && a.vec_a && a.vec_b && (!a.trans_a || a.M % 8 == 0) &&
+         (!a.trans_b || a.N % 8 == 0) && !a.force_big && a.fast >= 0 &&
+         (!a.trans_a || a.K * a.lda * 2 < (1LL << 32)) && (!a.trans_b || a.K * a.ldb * 2 < (1LL << 32));
+}
+
+extern "C" long long dtp_gemm_workspace(const DtpGemmArgs* in) {
+  if (!in || in->splitk != 0 || in->M <= 0 || in->N <= 0 || in->K <= 0) return 0;
+  DtpGemmArgs a = *in;
+  a.vec_a = (a.lda % 8 == 0) && aligned16(a.A);
+  a.vec_b = (a.ldb % 8 == 0) && aligned16(a.B);
+  if (!ph8_shape(a)) return 0;
+  const int sp = gemm::ph8_split_plan(a);
+  return sp > 1 ? gemm::ph8_split_bytes(a, sp) : 0;
+}
+
 extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   if (!in) return set_err(1, "dtp_gemm: null args");
   DtpGemmArgs a = *in;
@@ -1178,17 +1008,25 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
       return check_launch("dtp_gemm(skinny output)");
     }
   }
+  const bool auto_split = a.splitk == 0;  // 0: the 8-phase split-K plan when it applies, else no split
   if (a.splitk < 1) a.splitk = 1;
   if (a.splitk > 1 && (a.out_dtype != DTP_DT_F32 || a.act || a.aux))
     return set_err(1, "dtp_gemm: split-K needs an f32 output and no activation epilogue");
   const int epc = a.dtype == DTP_DT_BF16 ? 8 : 4;
   a.vec_a = (a.lda % epc == 0) && aligned16(a.A);
   a.vec_b = (a.ldb % epc == 0) && aligned16(a.B);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (auto_split && ph8_shape(a)) {
+    const int sp = gemm::ph8_split_plan(a);
+    if (sp > 1 && a.work && a.work_bytes >= gemm::ph8_split_bytes(a, sp)) {
+      a.splitk = sp;
+      return gemm::launch_ph8(a, s, -1);
+    }
+  }
   const int tm = (a.M + gemm::kBM - 1) / gemm::kBM, tn = (a.N + gemm::kBN - 1) / gemm::kBN;
   const int bk = a.dtype == DTP_DT_BF16 ? 64 : 32;
   const int ktiles = (a.K + bk - 1) / bk;
   if (a.splitk > ktiles) a.splitk = ktiles;
-  hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.splitk > 1 && !a.accumulate) {  // atomics accumulate into C: clear it first
     hipError_t e = hipMemset2DAsync(a.C, sizeof(float) * static_cast<size_t>(a.ldc), 0, sizeof(float) * a.N, a.M, s);
     if (e != hipSuccess) return set_err(2, "dtp_gemm: clearing the split-K output failed");
@@ -1225,8 +1063,12 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   const bool fast_shape = a.dtype == DTP_DT_BF16 && a.splitk == 1 && a.K % 64 == 0 && a.vec_a && a.vec_b &&
                           (!a.trans_a || a.M % 8 == 0) && (!a.trans_b || a.N % 8 == 0) && !a.force_big;
   if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
-    const int var = a.fast >= 2 ? (a.fast - 2) & 31 : gemm::kFastDefaultVar;
+    // default: the 8-phase kernel (gemm_ph8.hip)
+    if (a.fast < 2 && ph8_shape(a)) return gemm::launch_ph8(a, s, -1);
+    const int var = a.fast >= 2 ? a.fast - 2 : gemm::kFastDefaultVar;
     switch (var) {
+      case 32: return gemm::launch_ph8(a, s, 0);  // 8-phase, balanced reads (gemm_ph8.hip)
+      case 34: return gemm::launch_ph8(a, s, 2);  // 8-phase, reads 12/4/8/0 per phase (A/B)
       case 0: return gemm::launch_fast<0>(a, s);
       case 1: return gemm::launch_fast<1>(a, s);
       case 2: return gemm::launch_fast<2>(a, s);

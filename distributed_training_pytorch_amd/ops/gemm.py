@@ -17,16 +17,18 @@ On CPU tensors every function runs the PyTorch reference of the same math (the
 gloo test paths); on a GPU the HIP kernels are required.
 
 Backend for large bf16 problems (``DTP_GEMM_BACKEND`` / ``set_backend``):
-``blaslt`` (default) runs the GEMM on hipBLASLt (``torch.mm``/``addmm``, fp32
-output through ``out_dtype``) with the epilogue as one extra in-place elementwise
-pass; ``mfma`` always runs the kernels above; ``auto`` times both once per problem
+``mfma`` (default) always runs the kernels above -- the 256x256 bf16 layer GEMMs on
+the eight-phase LDS-DMA kernel (``csrc/gemm_ph8.hip``), few-tile long-K problems
+(the weight gradient of a <= 2048-wide layer) on its split-K plan.  Measured end to
+end (``profiles/gemm_r3_ph8/``) it is the fastest of the three on the 1024/2048/4096-
+wide MLPs: 1.30 / 1.81 / 4.77 ms per step vs 1.62 / 1.82 / 4.86 with hipBLASLt and
+2.26 / 2.31 / 5.77 stock.  ``blaslt`` runs the GEMM on hipBLASLt (``torch.mm``/
+``addmm``, fp32 output through ``out_dtype``) with the epilogue as one extra in-place
+elementwise pass -- an A/B reference only; ``auto`` times both once per problem
 signature (scratch outputs, events) and keeps hipBLASLt only when it is at least
-``_TUNE_MARGIN`` faster.  Measured end to end (``profiles/wide_r2/``), hipBLASLt for
-every large layer GEMM is the fastest of the three on the 1024/2048/4096-wide MLPs
-(1.73 / 2.00 / 5.42 ms per step vs 1.89 / 2.90 / 6.39 all-MFMA); the isolated
-per-problem timings of ``auto`` under-predict that gain.  Calls that pin a kernel
-(``fast`` / ``splitk`` / ``force_big``), fp32 operands, ``alpha != 1``, K <= 16,
-N or M == 1 and problems under ``_TUNE_MIN_FLOP`` always run the MFMA kernels.
+``_TUNE_MARGIN`` faster.  Calls that pin a kernel (``fast`` / ``splitk`` /
+``force_big``), fp32 operands, ``alpha != 1``, K <= 16, N or M == 1 and problems
+under ``_TUNE_MIN_FLOP`` always run the MFMA kernels.
 """
 from __future__ import annotations
 
@@ -40,7 +42,7 @@ from .. import _native as nat
 _DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16}
 _BM = 128
 _BACKENDS = ("auto", "mfma", "blaslt")
-_backend = os.environ.get("DTP_GEMM_BACKEND", "blaslt")
+_backend = os.environ.get("DTP_GEMM_BACKEND", "mfma")
 if _backend not in _BACKENDS:
     raise ValueError(f"DTP_GEMM_BACKEND={_backend!r}: expected one of {_BACKENDS}")
 _TUNE_MIN_FLOP = 4e9      # below this the fused kernel (no extra epilogue pass) is kept
@@ -141,8 +143,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
 
 def _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, out, bias, aux, act, slope, accumulate, alpha, splitk,
                  out_dtype, force_big, fast):
-    if splitk is None:
-        splitk = _auto_splitk(M, N, K, a.dtype) if (out_dtype == torch.float32 and not act and aux is None) else 1
+    split_ok = out_dtype == torch.float32 and not act and aux is None
     if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
         bias = bias.float().contiguous()
     args = nat.GemmArgs()
@@ -154,11 +155,26 @@ def _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, out, bias, aux, act, slop
     args.M, args.N, args.K = M, N, K
     args.dtype, args.out_dtype = _DT[a.dtype], _DT[out_dtype]
     args.trans_a, args.trans_b = int(trans_a), int(trans_b)
-    args.act, args.accumulate, args.splitk = int(act), int(accumulate), int(splitk)
+    args.act, args.accumulate = int(act), int(accumulate)
     args.alpha, args.slope = float(alpha), float(slope)
     args.force_big = int(force_big)
     # int >= 2: force the fast kernel with schedule variant fast - 2 (experiments / benches)
     args.fast = 0 if fast is None else (int(fast) if fast is not True and fast is not False else (1 if fast else -1))
+    work = None
+    if splitk is None and split_ok:
+        # few output tiles, long K (the weight gradient of a <= 2048-wide layer): the
+        # library's 8-phase split-K plan, partial sums in a workspace from torch's
+        # caching allocator (stream-ordered, hipGraph-capturable); else the classic
+        # kernel's atomic split-K
+        args.splitk = 0
+        nbytes = lib.dtp_gemm_workspace(args)
+        if nbytes > 0:
+            work = torch.empty(nbytes, dtype=torch.uint8, device=out.device)
+            args.work, args.work_bytes = work.data_ptr(), nbytes
+        else:
+            splitk = _auto_splitk(M, N, K, a.dtype)
+    if work is None:
+        args.splitk = int(splitk if splitk is not None else 1)
     nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
     return out
 

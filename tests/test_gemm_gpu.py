@@ -74,8 +74,8 @@ def test_gemm_bf16_big_tile_kernel(ta, tb):
 
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
-@pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192)])
-@pytest.mark.parametrize("kernel", [True, 2, 3, 8])  # default, variants 0, 1, 6 (direct epilogue; fast = 2 + variant)
+@pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192), (1288, 776, 512)])
+@pytest.mark.parametrize("kernel", [True, 2, 3, 8, 34, 35, 36])  # default, variants 0, 1, 6 (direct epilogue), 8-phase: balanced staggered / lockstep, unbalanced (fast = 2 + variant)
 def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     """The LDS-DMA 256x256 kernel (row images + transposing LDS reads): every layout,
     ragged M/N edges, bias / LeakyReLU' (aux) epilogues, f32 and bf16 outputs."""
@@ -94,7 +94,7 @@ def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
 
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
-@pytest.mark.parametrize("kernel", [True, 8])  # LDS-staged vector epilogue (default) and the direct one
+@pytest.mark.parametrize("kernel", [True, 8, 34])  # LDS-staged vector epilogue (default), the direct one, 8-phase
 def test_gemm_bf16_fast_kernel_accumulate_epilogues(ta, tb, kernel):
     """Epilogue operands of the LDS-DMA kernel: accumulate into f32 (the in-place weight
     gradient) and bf16 outputs, alpha + bias + LeakyReLU, and an output view whose rows
@@ -291,3 +291,27 @@ def test_gemm_skinny_output_weight_grad(M, N, K):
     old = torch.randn(M, N, device=DEV)
     c = gemm(a, b, trans_a=True, trans_b=True, out=old.clone(), accumulate=True, alpha=0.5)
     torch.testing.assert_close(c, 0.5 * ref + old, rtol=1e-4, atol=1e-3 * K ** 0.5)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape", [(512, 512, 4096), (520, 264, 2048), (1024, 1024, 16384)])
+def test_gemm_bf16_ph8_split_k(ta, tb, shape):
+    """Few output tiles and a long K (the weight gradient of a <= 2048-wide layer): the
+    8-phase kernel's split-K plan -- K-slices into a workspace, one reduction pass with
+    the epilogue (accumulate, alpha, bias) -- against the fp32 reference."""
+    from distributed_training_pytorch_amd import _native as nat
+    M, N, K = shape
+    a, b = _ops(M, N, K, ta, tb, torch.bfloat16, 17)
+    ref = _ref(a, b, ta, tb)
+    args = nat.GemmArgs()
+    args.A, args.B, args.M, args.N, args.K = a.data_ptr(), b.data_ptr(), M, N, K
+    args.lda, args.ldb = a.stride(0), b.stride(0)
+    args.dtype, args.out_dtype, args.trans_a, args.trans_b = nat.DT_BF16, nat.DT_F32, int(ta), int(tb)
+    assert nat.load().dtp_gemm_workspace(args) > 0  # the plan applies to these shapes
+    old = torch.randn(M, N, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    c = gemm(a, b, trans_a=ta, trans_b=tb, out=old.clone(), accumulate=True, alpha=0.5, bias=bias)
+    torch.testing.assert_close(c, old + 0.5 * ref + bias, rtol=1e-4, atol=2e-3 * K ** 0.5)
+    c2 = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
+    torch.testing.assert_close(c2, ref, rtol=1e-4, atol=2e-3 * K ** 0.5)
