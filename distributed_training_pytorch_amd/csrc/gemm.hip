@@ -401,61 +401,6 @@ DTP_DEV bf16x8 fast_frag(const char* img, const int* off, int f, int ks) {
   }
 }
 
-// Epilogue of the 256x256 LDS-DMA kernels: acc[i][j][r] = C(row wr*128 + 16 i +
-// 4 lg + r, col wc*64 + 16 j + lr).  Per fragment row i, the 16 activation-gradient
-// operands (aux) are requested together (clamped, unconditional loads) before any
-// is used: 8 load round trips per lane instead of one per element.
-DTP_DEV void fast_epilogue(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc, int lr,
-                           int lg) {
-  char* C = static_cast<char*>(a.C);
-  const uint16_t* aux = static_cast<const uint16_t*>(a.aux);
-  float bias[4];
-  int ncol[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    ncol[j] = n0 + wc * 64 + 16 * j + lr;
-    bias[j] = (a.bias && ncol[j] < a.N) ? a.bias[ncol[j]] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int mrow = m0 + wr * 128 + 16 * i + 4 * lg;
-    float gate[4][4];
-    if (aux) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          gate[j][r] = bf16_to_f32(aux[static_cast<long long>(min(mrow + r, a.M - 1)) * a.ldaux + min(ncol[j], a.N - 1)]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gate[j][r] = leaky_grad_from_out(gate[j][r], a.slope);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mrow + r, n = ncol[j];
-        if (m >= a.M || n >= a.N) continue;
-        float v = a.alpha * acc[i][j][r] + bias[j];
-        if (aux) v *= gate[j][r];
-        if (a.act) v = leaky(v, a.slope);
-        const long long off = static_cast<long long>(m) * a.ldc + n;
-        if (a.out_dtype == DTP_DT_BF16) {
-          uint16_t* p = reinterpret_cast<uint16_t*>(C) + off;
-          if (a.accumulate) v += bf16_to_f32(*p);
-          *p = f32_to_bf16(v);
-        } else {
-          float* p = reinterpret_cast<float*>(C) + off;
-          if (a.accumulate) v += *p;
-          *p = v;
-        }
-      }
-    }
-  }
-}
-
-
 DTP_DEV void fast_epilogue_lds(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], char* lds, int m0, int n0, int wave,
                                int wr, int wc, int lane) {
   float* buf = reinterpret_cast<float*>(lds) + wave * kEpiWaveFloats;
@@ -469,11 +414,13 @@ DTP_DEV void fast_epilogue_lds(const DtpGemmArgs& a, const f32x4 (&acc)[8][4], c
   fast_epilogue_pass<1>(a, acc, buf, bias, m0 + wr * 128 + 64, ncol, vec, lane);
 }
 
-// VAR (schedule experiments, selected by DtpGemmArgs::fast = 2 + VAR): bit 0 = static
-// s_setprio(1) for waves 4-7 instead of per-cluster flips; bit 1 = the next tile's
-// DMA split over the two k-steps (4 pieces ahead of each MFMA cluster); bit 2 = the
-// direct per-element epilogue instead of the LDS-staged one
-template <bool TA, bool TB, int VAR>
+// Schedule: the next tile's DMA split over the two k-steps (4 pieces ahead of each MFMA
+// cluster), per-cluster s_setprio.  The other round-1/2 schedule experiments (static
+// priority, unsplit DMA, direct epilogue, one wave per SIMD, the no-DMA / no-MFMA
+// diagnostics) lost to this one and were removed in round 3 (profiles/gemm_r1_fast).
+// Since round 3 the 8-phase kernel (gemm_ph8.hip) is the default; this one serves the
+// shapes it cannot take (a transposed operand spanning >= 4 GiB) and A/B runs.
+template <bool TA, bool TB>
 __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64;
   // [buffer][A | B] images: 128 KiB; after the K loop, 8 waves x 64 x 68 f32 epilogue staging (136 KiB)
@@ -510,23 +457,13 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr bool kStaticPrio = VAR & 1, kSplitDma = VAR & 2;
-  // diagnostics only (wrong results; gemm_variants.py timing): bit 3 = no DMA after the
-  // first tile (MFMA + LDS reads alone), bit 4 = no MFMA (DMA + barriers alone)
-  constexpr bool kNoDma = VAR & 8, kNoMfma = VAR & 16;
-  if constexpr (kStaticPrio) {
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
   stage(0, 0, 0, 4);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const bool more = kt + 1 < nk;
-    if (more && !kNoDma) {
-      if constexpr (kSplitDma) stage(buf ^ 1, kt + 1, 0, 2);
-      else stage(buf ^ 1, kt + 1, 0, 4);
-    }
+    if (more) stage(buf ^ 1, kt + 1, 0, 2);
     const char* ia = lds + buf * 2 * kFastImg;
     const char* ib = ia + kFastImg;
 #pragma unroll
@@ -536,169 +473,29 @@ __global__ __launch_bounds__(kFastThreads) void gemm_fast_kernel(DtpGemmArgs a) 
       for (int j = 0; j < 4; ++j) fb[j] = fast_frag<TB>(ib, offB, j, ks);
 #pragma unroll
       for (int i = 0; i < 8; ++i) fa[i] = fast_frag<TA>(ia, offA, i, ks);
-      if constexpr (kSplitDma && !kNoDma) {
-        if (ks == 1 && more) stage(buf ^ 1, kt + 1, 2, 4);
-      }
-      if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(1);
-      if constexpr (!kNoMfma) {
+      if (ks == 1 && more) stage(buf ^ 1, kt + 1, 2, 4);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
-      if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  if constexpr (VAR & 4) fast_epilogue(a, acc, m0, n0, wr, wc, lr, lg);  // direct per-element stores (A/B)
-  else fast_epilogue_lds(a, acc, lds, m0, n0, wave, wr, wc, lane);
+  fast_epilogue_lds(a, acc, lds, m0, n0, wave, wr, wc, lane);
 }
 
-// ---------------------------------------------------------------------------
-// One-wave-per-SIMD variant: 4 waves (2 x 2), each a 128x128 sub-tile (64
-// accumulators of 16x16x32 MFMAs = 256 registers: the unified VGPR/AGPR file at one
-// wave per SIMD).  The same LDS-DMA images, swizzles and fragment reads as above,
-// but the wave pipelines its own LDS reads instead of relying on a second wave:
-//   k-step 1's 16 fragment reads are in flight during k-step 0's 64 MFMAs; the
-//   per-tile barrier sits between the two k-steps, and right after it the NEXT
-//   tile's k-step-0 reads are issued, so they land during k-step 1's MFMAs.
-//   The DMA of tile t+2 goes out right after that barrier (its buffer was just
-//   released), one whole tile ahead of its use.
-// ---------------------------------------------------------------------------
-constexpr int kW4Threads = 256;
-
-template <bool TRANS>
-DTP_DEV void w4_sources(const char* (&src)[8], const char* base, long long ld, int r0, int R, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int q = 4 * i + wave;  // the 1-KiB chunk of the image this instruction fills
-    if constexpr (!TRANS) {
-      const int row = q * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ fswz(row);
-      const int rr = min(r0 + row, R - 1);
-      src[i] = base + (static_cast<long long>(rr) * ld + c * 8) * 2;
-    } else {
-      const int k = q * 2 + (lane >> 5);
-      const int c = (lane & 31) ^ (fswz(k) << 1);
-      const int col = min(r0 + c * 8, R - 8);
-      src[i] = base + (static_cast<long long>(k) * ld + col) * 2;
-    }
-  }
-}
-
-template <bool TA, bool TB>
-__global__ __launch_bounds__(kW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(DtpGemmArgs a) {
-  constexpr int BK = 64;
-  __shared__ __align__(16) char lds[2 * 2 * kFastImg];  // 128 KiB; epilogue: 4 x 17 KiB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const TileId id = decode_tile<256, 256>(a);
-  const int m0 = id.m0, n0 = id.n0, nk = a.K / BK;
-
-  const char* srcA[8];
-  const char* srcB[8];
-  w4_sources<TA>(srcA, static_cast<const char*>(a.A), a.lda, m0, a.M, wave, lane);
-  w4_sources<TB>(srcB, static_cast<const char*>(a.B), a.ldb, n0, a.N, wave, lane);
-  const long long kbA = TA ? static_cast<long long>(BK) * a.lda * 2 : BK * 2;
-  const long long kbB = TB ? static_cast<long long>(BK) * a.ldb * 2 : BK * 2;
-  auto stage = [&](int buf, int kt) {
-    char* img = lds + buf * 2 * kFastImg;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcA[i] + kt * kbA), (lds_void_t*)(img + (4 * i + wave) * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[i] + kt * kbB),
-                                       (lds_void_t*)(img + kFastImg + (4 * i + wave) * 1024), 16, 0, 0);
-    }
-  };
-  int offA[TA ? 8 : 2], offB[TB ? 8 : 2];
-  fast_offsets<TA, 8>(offA, wr * 128, lane);
-  fast_offsets<TB, 8>(offB, wc * 128, lane);
-  auto frags = [&](int buf, int ks, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
-    const char* ia = lds + buf * 2 * kFastImg;
-    const char* ib = ia + kFastImg;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fb[j] = fast_frag<TB>(ib, offB, j, ks);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = fast_frag<TA>(ia, offA, i, ks);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed, tile 1 may still fly
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-  frags(0, 0, fa0, fb0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    frags(buf, 1, fa1, fb1);  // k-step 1 reads fly during k-step 0's MFMAs
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
-    // every read of `buf` has returned and tile kt+1's DMA (issued one tile ago) has landed
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 2 < nk) stage(buf, kt + 2);
-    if (kt + 1 < nk) frags(buf ^ 1, 0, fa0, fb0);  // next tile's k-step 0 flies during k-step 1's MFMAs
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave is done with the operand images: they become epilogue staging
-
-  float* ebuf = reinterpret_cast<float*>(lds) + wave * kEpiWaveFloats;
-  const uintptr_t cp = reinterpret_cast<uintptr_t>(a.C), ap = reinterpret_cast<uintptr_t>(a.aux);
-  const bool aligned = a.ldc % 8 == 0 && (cp & 15) == 0 && (!a.aux || (a.ldaux % 8 == 0 && (ap & 15) == 0));
-  auto half = [&](auto JH) {
-    constexpr int jh = decltype(JH)::value;
-    const int ncol = n0 + wc * 128 + 64 * jh + 8 * (lane & 7);
-    const bool vec = aligned && ncol + 8 <= a.N;
-    float bias[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) bias[c] = (a.bias && ncol + c < a.N) ? a.bias[ncol + c] : 0.f;
-    fast_epilogue_pass<0, 4 * jh, 8>(a, acc, ebuf, bias, m0 + wr * 128, ncol, vec, lane);
-    fast_epilogue_pass<1, 4 * jh, 8>(a, acc, ebuf, bias, m0 + wr * 128 + 64, ncol, vec, lane);
-  };
-  half(std::integral_constant<int, 0>{});
-  half(std::integral_constant<int, 1>{});
-}
-
-int launch_w4(const DtpGemmArgs& a, hipStream_t s) {
-  const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
-  const dim3 gf((unsigned)tiles), bf(kW4Threads);
-  switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
-    case 0: hipLaunchKernelGGL((gemm_w4_kernel<false, false>), gf, bf, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((gemm_w4_kernel<false, true>), gf, bf, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((gemm_w4_kernel<true, false>), gf, bf, 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_w4_kernel<true, true>), gf, bf, 0, s, a); break;
-  }
-  return check_launch("dtp_gemm(LDS-DMA 256x256, 4 waves)");
-}
-
-constexpr int kFastDefaultVar = 2;  // two-buffer kernel's schedule when the 8-phase one cannot run: next tile's DMA split over the
-                                     // k-steps, +0.3-5 % over var 1 (profiles/gemm_r1_fast/variants_ring.jsonl)
-
-template <int VAR>
 int launch_fast(const DtpGemmArgs& a, hipStream_t s) {
   const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
   const dim3 gf((unsigned)tiles), bf(kFastThreads);
   switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
-    case 0: hipLaunchKernelGGL((gemm_fast_kernel<false, false, VAR>), gf, bf, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((gemm_fast_kernel<false, true, VAR>), gf, bf, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((gemm_fast_kernel<true, false, VAR>), gf, bf, 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_fast_kernel<true, true, VAR>), gf, bf, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((gemm_fast_kernel<false, false>), gf, bf, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((gemm_fast_kernel<false, true>), gf, bf, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_fast_kernel<true, false>), gf, bf, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_fast_kernel<true, true>), gf, bf, 0, s, a); break;
   }
   return check_launch("dtp_gemm(LDS-DMA 256x256)");
 }
@@ -1065,18 +862,12 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
   if (fast_shape && a.fast >= 0 && (a.fast > 0 || big_tiles >= 128)) {
     // default: the 8-phase kernel (gemm_ph8.hip)
     if (a.fast < 2 && ph8_shape(a)) return gemm::launch_ph8(a, s, -1);
-    const int var = a.fast >= 2 ? a.fast - 2 : gemm::kFastDefaultVar;
-    switch (var) {
+    // fast = 2 + variant pins a kernel (A/B runs, tests): 32 / 34 the 8-phase schedules,
+    // anything else the two-buffer kernel
+    switch (a.fast - 2) {
       case 32: return gemm::launch_ph8(a, s, 0);  // 8-phase, balanced reads (gemm_ph8.hip)
-      case 34: return gemm::launch_ph8(a, s, 2);  // 8-phase, reads 12/4/8/0 per phase (A/B)
-      case 0: return gemm::launch_fast<0>(a, s);
-      case 1: return gemm::launch_fast<1>(a, s);
-      case 2: return gemm::launch_fast<2>(a, s);
-      case 6: return gemm::launch_fast<6>(a, s);  // var 2 with the direct per-element epilogue (A/B)
-      case 7: return gemm::launch_w4(a, s);  // one wave per SIMD, 128x128 per wave
-      case 10: return gemm::launch_fast<10>(a, s);  // diagnostics: var 2 without DMA
-      case 18: return gemm::launch_fast<18>(a, s);  // diagnostics: var 2 without MFMA
-      default: return gemm::launch_fast<3>(a, s);
+      case 34: return gemm::launch_ph8(a, s, 2);  // 8-phase, reads 12/4/8/0 per phase
+      default: return gemm::launch_fast(a, s);    // two-buffer LDS-DMA kernel
     }
   }
   // lean loads need every row 16-byte aligned and whole 8-element chunks

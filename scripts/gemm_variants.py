@@ -1,8 +1,8 @@
 """A/B the fast GEMM's schedule variants in ONE process, interleaved rounds
 (cdna_hip_programming.md §5.4 rule 24). usage: python scripts/gemm_variants.py [rounds]
 
-VARIANTS=var2,var10,var18,torch  selects variants (fast = 2 + N); N >= 8 are
-diagnostic kernels (no DMA / no MFMA) whose results are not checked.
+VARIANTS=var2,var32,var34,torch  selects variants (fast = 2 + N): var2 the two-buffer
+kernel, var32 / var34 the 8-phase kernel with balanced / unbalanced reads.
 SHAPES=wide  times the wide-MLP GEMMs (W=4096, batch 8192) instead of the squares."""
 import json
 import os
@@ -29,7 +29,7 @@ def t_ms(fn, iters=10):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    variants = os.environ.get("VARIANTS", "var0,var1,var2,var3,torch").split(",")
+    variants = os.environ.get("VARIANTS", "var2,var32,var34,torch").split(",")
     shapes = [(4096, 4096, 4096, "NN"), (8192, 8192, 8192, "NN"), (8192, 8192, 8192, "TT"), (8192, 8192, 8192, "NT")]
     if os.environ.get("SHAPES") == "wide":  # forward, input gradient, weight gradient of a 4096-wide layer
         shapes = [(8192, 4096, 4096, "NN"), (8192, 4096, 4096, "NT"), (4096, 4096, 8192, "TT")]
@@ -49,7 +49,7 @@ def main():
                 fns[v] = (lambda k=k: gemm(a, b, trans_a=ta, trans_b=tb, out=out, fast=k))
                 fns[v]()
                 err = (out.float() - ref.float()).abs().max().item()
-                assert k - 2 >= 8 or err < 1.0, (v, err)
+                assert err < 1.0, (v, err)
         res = {v: [] for v in variants}
         for _ in range(rounds):
             for v in variants:

@@ -75,7 +75,7 @@ def test_gemm_bf16_big_tile_kernel(ta, tb):
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192), (1288, 776, 512)])
-@pytest.mark.parametrize("kernel", [True, 2, 3, 8, 34, 35, 36])  # default, variants 0, 1, 6 (direct epilogue), 8-phase: balanced staggered / lockstep, unbalanced (fast = 2 + variant)
+@pytest.mark.parametrize("kernel", [True, 4, 34, 36])  # default (8-phase by layout), two-buffer kernel, 8-phase balanced / unbalanced (fast = 2 + variant)
 def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     """The LDS-DMA 256x256 kernel (row images + transposing LDS reads): every layout,
     ragged M/N edges, bias / LeakyReLU' (aux) epilogues, f32 and bf16 outputs."""
@@ -94,7 +94,7 @@ def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
 
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
-@pytest.mark.parametrize("kernel", [True, 8, 34])  # LDS-staged vector epilogue (default), the direct one, 8-phase
+@pytest.mark.parametrize("kernel", [True, 4, 34])  # 8-phase default, two-buffer kernel, 8-phase balanced
 def test_gemm_bf16_fast_kernel_accumulate_epilogues(ta, tb, kernel):
     """Epilogue operands of the LDS-DMA kernel: accumulate into f32 (the in-place weight
     gradient) and bf16 outputs, alpha + bias + LeakyReLU, and an output view whose rows
