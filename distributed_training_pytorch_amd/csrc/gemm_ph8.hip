@@ -240,6 +240,13 @@ __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
     rdB(lds + 2 * kPart, fx);  // Bf(0): retired by the prologue wait
     auto tile = [&](auto ODD, int u, bf16x8 (&bf)[2][2], bf16x8 (&bs)[2][2]) {
       constexpr bool odd = decltype(ODD)::value;
+      // per-lane address state made opaque once per tile, so LICM cannot hoist every
+      // phase's DMA and fragment address out of the loop into live registers
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(oSA[i >> 1][i & 1]), "+v"(oSB[i >> 1][i & 1]));
+#pragma unroll
+      for (int i = 0; i < (TA ? 4 : 2); ++i) asm volatile("" : "+v"(oA[i]));
+      asm volatile("" : "+v"(oB[0]), "+v"(oB[1]));
       constexpr int pf = odd ? 3 : 2, ps = odd ? 2 : 3;  // this tile's Bf / Bs parts
       using QF = std::integral_constant<int, odd ? 1 : 0>;
       using QS = std::integral_constant<int, odd ? 0 : 1>;
@@ -407,15 +414,11 @@ long long ph8_split_bytes(const DtpGemmArgs& a, int splitk) { return 4LL * split
 int launch_ph8(const DtpGemmArgs& a, hipStream_t s, int variant) {
   const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.splitk;
   const dim3 g((unsigned)tiles), b(ph8::kThreads);
-  // default (-1) by layout, A/B in profiles/gemm_r3_ph8: the balanced reads win on NN
-  // and TT; on NT (dx = dz W) the balanced instance spills, the unbalanced one wins
-  if (variant < 0) variant = (!a.trans_a && a.trans_b) ? 2 : 0;
+  // default (-1): the balanced reads (profiles/gemm_r3_ph8)
+  if (variant < 0) variant = 0;
   if ((a.K / 64 / a.splitk) % 2) variant = 2;  // the balanced schedule runs K-tiles in pairs
-  // split-K launches take the unbalanced schedule: the balanced instance with the
-  // split epilogue crosses 256 VGPRs and spills inside the K loop
-  if (a.splitk > 1) launch_lay<false, true>(a, s, g, b);
-  else if (variant == 2) launch_lay<false, false>(a, s, g, b);
-  else launch_lay<true, false>(a, s, g, b);
+  if (a.splitk > 1) variant == 2 ? launch_lay<false, true>(a, s, g, b) : launch_lay<true, true>(a, s, g, b);
+  else variant == 2 ? launch_lay<false, false>(a, s, g, b) : launch_lay<true, false>(a, s, g, b);
   if (a.splitk > 1) {
     int e = check_launch("dtp_gemm(8-phase LDS-DMA 256x256, split-K)");
     if (e) return e;

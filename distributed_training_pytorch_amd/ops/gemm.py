@@ -21,8 +21,8 @@ Backend for large bf16 problems (``DTP_GEMM_BACKEND`` / ``set_backend``):
 the eight-phase LDS-DMA kernel (``csrc/gemm_ph8.hip``), few-tile long-K problems
 (the weight gradient of a <= 2048-wide layer) on its split-K plan.  Measured end to
 end (``profiles/gemm_r3_ph8/``) it is the fastest of the three on the 1024/2048/4096-
-wide MLPs: 1.30 / 1.81 / 4.77 ms per step vs 1.62 / 1.82 / 4.86 with hipBLASLt and
-2.26 / 2.31 / 5.77 stock.  ``blaslt`` runs the GEMM on hipBLASLt (``torch.mm``/
+wide MLPs: 1.30 / 1.81 / 4.64 ms per step vs 1.63 / 1.92 / 4.90 with hipBLASLt and
+2.47 / 2.32 / 5.82 stock.  ``blaslt`` runs the GEMM on hipBLASLt (``torch.mm``/
 ``addmm``, fp32 output through ``out_dtype``) with the epilogue as one extra in-place
 elementwise pass -- an A/B reference only; ``auto`` times both once per problem
 signature (scratch outputs, events) and keeps hipBLASLt only when it is at least
