@@ -751,12 +751,14 @@ using namespace dtp;
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // the 8-phase kernel's preconditions (bf16, whole 64-deep K-tiles, 16-byte aligned rows,
-// a transposed operand in whole 8-element chunks); its per-K-tile DMA offsets are
-// 32-bit, so a transposed operand's K rows must span < 4 GiB
+// a transposed operand in whole 8-element chunks); its DMA offsets are 32-bit: a
+// transposed operand's K rows, and a K-contiguous operand's 256 tile rows, must span
+// < 4 GiB
 static bool ph8_shape(const DtpGemmArgs& a) {
   return a.dtype == DTP_DT_BF16 && a.K % 64 == 0 && a.vec_a && a.vec_b && (!a.trans_a || a.M % 8 == 0) &&
          (!a.trans_b || a.N % 8 == 0) && !a.force_big && a.fast >= 0 &&
-         (!a.trans_a || a.K * a.lda * 2 < (1LL << 32)) && (!a.trans_b || a.K * a.ldb * 2 < (1LL << 32));
+         (a.trans_a ? a.K * a.lda * 2 : 256 * a.lda * 2) < (1LL << 32) &&
+         (a.trans_b ? a.K * a.ldb * 2 : 256 * a.ldb * 2) < (1LL << 32);
 }
 
 extern "C" long long dtp_gemm_workspace(const DtpGemmArgs* in) {

@@ -17,12 +17,21 @@
 //    (qm, qn) of 4 x 2 fragments.  Quadrant qm of every wave lives in the operand
 //    PART A_qm = tile rows [128 qm, +128), quadrant qn in B_qn = tile columns
 //    [128 qn, +128): each of the four parts is read in exactly one phase per tile.
-//  * one K-tile = 4 phases, one quadrant (16 MFMAs = 256 matrix cycles) each:
+//  * one K-tile = 4 phases, one quadrant (16 MFMAs = 256 matrix cycles) each.  The
+//    simple schedule (variant 2) reads 12 / 4 / 8 / 0 fragments per phase:
 //        phase 0: read A0 + B0 fragments, MFMA quadrant (0,0), DMA A0 of tile u+1
 //        phase 1: read B1,               MFMA (0,1),            DMA B1 of tile u+1
 //        phase 2: read A1,               MFMA (1,1),            DMA A1 of tile u+1
 //        phase 3: (registers only),      MFMA (1,0),            DMA B0 of tile u+2
-//    Registers: 128 accumulators + A quadrant (32) + both B quadrants (32).
+//    The default (balanced) schedule reads 8 / 4 / 8 / 4: phase 3 pre-reads the next
+//    tile's first B part into the register set phase 2 released, so a tile's two B
+//    quadrants alternate between register sets and the K loop runs tiles in pairs.
+//    Registers: 128 accumulators + A quadrant (32) + both B quadrants (32); the lane
+//    address state is made opaque once per tile so LICM cannot hoist every phase's
+//    addresses into live registers (it spilled the balanced instances).
+//  * split-K (few output tiles, long K: launch_ph8 with splitk > 1): each block runs
+//    a K-slice and stores raw f32 partials to a workspace; splitk_reduce_kernel sums
+//    the slices and applies the epilogue.
 //  * LDS: 2 K-tile buffers x 4 parts x 16 KiB = 128 KiB, plus one 16 KiB sink
 //    for the DMA slots past the last tile (so every phase issues exactly one part
 //    and the wait count never changes).
@@ -345,35 +354,37 @@ __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
 }
 
 // C = alpha * sum_s work[s] + bias (+ C): the epilogue of a split-K launch (f32 out,
-// no activation); 4 columns per thread, 16-byte loads when the rows allow
+// no activation).  Block = one output row x 1024 columns, 4 columns per thread (one
+// 16-byte load per slice, contiguous per wave); the slices are read four at a time
+// with all loads issued before any add.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(DtpGemmArgs a) {
-  const int n4 = (a.N + 3) / 4;
-  const long long total = static_cast<long long>(a.M) * n4;
+  const int m = blockIdx.y, n = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (n >= a.N) return;
   const long long plane = static_cast<long long>(a.M) * a.N;
-  const float* w = static_cast<const float*>(a.work);
-  float* C = static_cast<float*>(a.C);
-  const bool vec = a.N % 4 == 0 && a.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
-    const int m = static_cast<int>(i / n4), n = static_cast<int>(i % n4) * 4;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (vec) {
-      for (int s = 0; s < a.splitk; ++s) {
-        const float4 x = *reinterpret_cast<const float4*>(w + s * plane + static_cast<long long>(m) * a.N + n);
-        v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
-      }
-      float4* cp = reinterpret_cast<float4*>(C + static_cast<long long>(m) * a.ldc + n);
-      float4 o = a.accumulate ? *cp : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float b0 = a.bias ? a.bias[n] : 0.f, b1 = a.bias ? a.bias[n + 1] : 0.f;
-      const float b2 = a.bias ? a.bias[n + 2] : 0.f, b3 = a.bias ? a.bias[n + 3] : 0.f;
-      o.x += a.alpha * v[0] + b0; o.y += a.alpha * v[1] + b1; o.z += a.alpha * v[2] + b2; o.w += a.alpha * v[3] + b3;
-      *cp = o;
-    } else {
-      for (int c = 0; c < 4 && n + c < a.N; ++c) {
-        float x = 0.f;
-        for (int s = 0; s < a.splitk; ++s) x += w[s * plane + static_cast<long long>(m) * a.N + n + c];
-        float* cp = C + static_cast<long long>(m) * a.ldc + n + c;
-        *cp = (a.accumulate ? *cp : 0.f) + a.alpha * x + (a.bias ? a.bias[n + c] : 0.f);
-      }
+  const float* w = static_cast<const float*>(a.work) + static_cast<long long>(m) * a.N + n;
+  float* c = static_cast<float*>(a.C) + static_cast<long long>(m) * a.ldc + n;
+  const bool vec = n + 4 <= a.N && a.N % 4 == 0 && a.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
+  if (vec) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 4 <= a.splitk; s += 4) {
+      f32x4 x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = *reinterpret_cast<const f32x4*>(w + (s + q) * plane);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v += x[q];
+    }
+    for (; s < a.splitk; ++s) v += *reinterpret_cast<const f32x4*>(w + s * plane);  // splitk = 2
+    f32x4* cv = reinterpret_cast<f32x4*>(c);
+    f32x4 o = {0.f, 0.f, 0.f, 0.f}, b = o;
+    if (a.accumulate) o = *cv;
+    if (a.bias) b = f32x4{a.bias[n], a.bias[n + 1], a.bias[n + 2], a.bias[n + 3]};
+    *cv = o + (a.alpha * v + b);  // the order of the unsplit epilogue: C + (alpha acc + bias)
+  } else {
+    for (int q = 0; q < 4 && n + q < a.N; ++q) {
+      float x = 0.f;
+      for (int s = 0; s < a.splitk; ++s) x += w[s * plane + q];
+      c[q] = (a.accumulate ? c[q] : 0.f) + (a.alpha * x + (a.bias ? a.bias[n + q] : 0.f));
     }
   }
 }
@@ -422,8 +433,7 @@ int launch_ph8(const DtpGemmArgs& a, hipStream_t s, int variant) {
   if (a.splitk > 1) {
     int e = check_launch("dtp_gemm(8-phase LDS-DMA 256x256, split-K)");
     if (e) return e;
-    const long long n = (long long)a.M * ((a.N + 3) / 4);
-    hipLaunchKernelGGL(ph8::splitk_reduce_kernel, dim3((unsigned)std::min<long long>((n + 255) / 256, 4096)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ph8::splitk_reduce_kernel, dim3((a.N + 1023) / 1024, a.M), dim3(256), 0, s, a);
     return check_launch("dtp_gemm(split-K reduction)");
   }
   return check_launch("dtp_gemm(8-phase LDS-DMA 256x256)");
