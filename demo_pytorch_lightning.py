@@ -43,6 +43,12 @@ class LitToyModel(LightningModule):
         self.log("loss/lossY", loss_y)
         return loss_x + loss_y
 
+    def fused_spec(self):
+        """What training_step computes, for the in-repo Trainer's fused train-step engine:
+        optimizer i trains models[i] on MSE(models[i](x), y) of the same batch (the
+        returned loss_X + loss_Y over two independent models), logged as metrics[i]."""
+        return {"models": [self.model_X, self.model_Y], "loss": "mse", "metrics": ["loss/lossX", "loss/lossY"]}
+
     def configure_optimizers(self):
         return [torch.optim.Adam(self.model_X.parameters(), lr=self.lr),
                 torch.optim.Adam(self.model_Y.parameters(), lr=self.lr)]
@@ -60,8 +66,11 @@ def get_args(argv=None):
     p.add_argument("--root_dir", type=str, default=None)
     p.add_argument("--no_progress", action="store_true")
     p.add_argument("--use_lightning", action="store_true", help="use pytorch_lightning if it is installed")
+    p.add_argument("--engine", default="auto", choices=["auto", "fused", "module"],
+                   help="in-repo Trainer: the fused train-step engine (from LitToyModel.fused_spec) or the "
+                        "per-batch nn.Module path (auto: fused when it applies)")
     p.add_argument("--no_graphs", action="store_true",
-                   help="in-repo Trainer: run every batch eagerly instead of replaying it as a hipGraph")
+                   help="in-repo Trainer, module path: run every batch eagerly instead of replaying it as a hipGraph")
     p.add_argument("--torch_optimizers", action="store_true",
                    help="in-repo Trainer: step the torch optimizers themselves, not the flat-optimizer kernel")
     p.add_argument("--precision", default="32", choices=["32", "bf16"],
@@ -89,8 +98,9 @@ def main(argv=None):
             TrainerCls = pl.Trainer
         except ImportError:
             print("pytorch_lightning not installed; using the in-repo Trainer", flush=True)
+    engine = "module" if (a.no_graphs or a.torch_optimizers) and a.engine == "auto" else a.engine
     extra = {"seed": a.seed, "use_graphs": not a.no_graphs, "native_optimizers": not a.torch_optimizers,
-             "every_n_train_steps": a.every_n_train_steps} if TrainerCls is Trainer else {}
+             "every_n_train_steps": a.every_n_train_steps, "engine": engine} if TrainerCls is Trainer else {}
     precision = 32 if a.precision == "32" else "bf16"
     trainer = TrainerCls(gpus=a.gpus, num_nodes=a.nnodes, max_steps=a.steps, precision=precision, accelerator=accel,
                          log_every_n_steps=min(50, len(dl) / a.batch_size), strategy="ddp",
@@ -105,7 +115,8 @@ def main(argv=None):
             steady = trainer.steady_steps * a.batch_size * getattr(trainer, "world_size", 1) / trainer.steady_time
         print(f"[Process 0] summary: {{'global_step': {trainer.global_step}, 'metrics': {trainer.callback_metrics}, "
               f"'checkpoint': {trainer.checkpoint_path!r}, 'samples_per_s': {sps}, 'steady_samples_per_s': {steady}, "
-              f"'graph_replays': {getattr(trainer, 'graph_replays', 0)}}}", flush=True)
+              f"'graph_replays': {getattr(trainer, 'graph_replays', 0)}, "
+              f"'engine': {getattr(trainer, 'engine_used', None)!r}}}", flush=True)
     if hasattr(trainer, "teardown"):
         trainer.teardown()
 

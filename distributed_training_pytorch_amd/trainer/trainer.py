@@ -170,7 +170,7 @@ class Trainer:
                  log_every_n_steps: float = 50, default_root_dir: str | None = None,
                  enable_checkpointing: bool = True, enable_progress_bar: bool = True, seed: int | None = None,
                  use_graphs: bool = True, native_optimizers: bool = True, every_n_train_steps: int = 0,
-                 **unused):
+                 engine: str = "auto", **unused):
         if precision in (32, "32", "32-true"):
             self.autocast_dtype = None
         elif precision in ("bf16", "bf16-mixed"):
@@ -202,6 +202,13 @@ class Trainer:
         # ModelCheckpoint(every_n_train_steps=N): also save ``last.ckpt`` every N batches
         # (what a restarted job resumes from, fit(ckpt_path="last"))
         self.every_n_train_steps = int(every_n_train_steps or 0)
+        # "auto": the fused train-step engine when the LightningModule declares its step
+        # (``fused_spec``) and everything it needs matches; "module": always the
+        # per-batch nn.Module path; "fused": the fused engine or an error
+        if engine not in ("auto", "fused", "module"):
+            raise ValueError(f"engine={engine!r}: auto, fused or module")
+        self.engine = engine
+        self.engine_used = "module"
         self._skip_batches = 0
         self._batch_in_epoch = 0
         self._log_dir = None
@@ -258,6 +265,9 @@ class Trainer:
         resume = self._resolve_ckpt(ckpt_path)
         if resume is not None:
             self._restore(model, opts, resume)
+        plan = self._fused_plan(model, opts, dl)
+        if plan is not None:
+            return self._fit_fused(model, opts, plan)
         # the flat gradient buffer of FlatDDP also serves one process: fused kernels add
         # their parameter gradients into its views in place (no AccumulateGrad adds)
         single_ok = self.device.type == "cuda" and all(
@@ -367,6 +377,156 @@ class Trainer:
             self._save(model, opts, final)
         logger.close()
         return self
+
+    # ------------------------------------------------------------------ fused engine
+    def _fused_plan(self, model, opts, dl):
+        """The fused train-step engine (engine/fused_trainer.py) runs the fit when the
+        LightningModule declares what its ``training_step`` computes --
+        ``fused_spec() -> {"models": [m_0, ...], "loss": "mse", "metrics": [name_0, ...]}``:
+        optimizer i trains ``models[i]`` (a ToyModel) on ``loss(models[i](x), y)`` of the
+        same batch -- and the rest matches: a GPU, plain Adam / SGD optimizers with one
+        param group over exactly one model's parameters each and equal hyperparameters,
+        a dataset with ``device_tensors``, precision 32 or bf16.  Otherwise None (the
+        per-batch module path); ``engine="fused"`` turns a mismatch into an error.
+
+        PL-1.5 semantics kept: each optimizer's update uses the gradient of its own
+        model's loss (the models are independent, so toggling the other optimizer's
+        parameters changes nothing), ``global_step`` counts batches, the
+        DistributedSampler order is exact at world > 1.  One difference in the logs:
+        every model's loss is its loss BEFORE this batch's update, where Lightning's
+        second ``training_step`` call would log the first model's post-update loss."""
+        from ..models.toy import ToyModel
+
+        if self.engine == "module":
+            return None
+
+        def no(why):
+            if self.engine == "fused":
+                raise RuntimeError(f"Trainer(engine='fused'): {why}")
+            return None
+
+        fs = getattr(model, "fused_spec", None)
+        fs = fs() if callable(fs) else None
+        if not fs:
+            return no("the LightningModule defines no fused_spec()")
+        if self.device.type != "cuda":
+            return no("the fused engine needs a GPU")
+        models, names = list(fs["models"]), list(fs.get("metrics") or [])
+        loss = fs.get("loss", "mse")
+        if loss not in ("mse", "ce") or len(names) != len(models) or len(opts) != len(models):
+            return no("fused_spec must name one metric per model and match one optimizer per model")
+        if not all(isinstance(m, ToyModel) for m in models) or any(m.spec != models[0].spec for m in models):
+            return no("fused_spec models must be ToyModels of one architecture")
+        cfgs = []
+        for o, m in zip(opts, models):
+            cfg = _optim_config(o)
+            ps = list(m.parameters())
+            if cfg is None or len(o.param_groups) != 1 or len(o.param_groups[0]["params"]) != len(ps) or \
+                    any(a is not b for a, b in zip(o.param_groups[0]["params"], ps)):
+                return no("each optimizer must be a plain Adam/SGD over exactly its model's parameters")
+            cfgs.append(cfg)
+        if any(c != cfgs[0] for c in cfgs):
+            return no("the optimizers' hyperparameters differ")
+        ds = getattr(dl, "dataset", None)
+        if not hasattr(ds, "device_tensors"):
+            return no("the dataset has no device_tensors()")
+        prec = "fp32" if self.autocast_dtype is None else "bf16"
+        return {"models": models, "names": names, "loss": loss, "optim": cfgs[0], "dataset": ds,
+                "batch": int(getattr(dl, "batch_size", None) or 1), "precision": prec, "spec": models[0].spec}
+
+    def _fit_fused(self, model, opts, plan):
+        from ..engine.fused_trainer import EngineConfig, FusedTrainer
+
+        models, names = plan["models"], plan["names"]
+        X, Y = plan["dataset"].device_tensors(self.device)
+        distributed = self.world_size > 1  # PL injects DistributedSampler(shuffle=True) under DDP
+        geom = SamplerGeometry(n=X.shape[0], world=self.world_size, rank=self.global_rank, batch=plan["batch"],
+                               shuffle=distributed, distributed=distributed, seed=0)
+        ecfg = EngineConfig(loss=plan["loss"], precision=plan["precision"])
+        tr = FusedTrainer(plan["spec"], len(models), X, Y, geom, plan["optim"], ecfg,
+                          init_params=[m.flat_params.detach() for m in models])
+        self._skip_batches = 0  # the engine positions its sampler from the step count
+        if self.global_step:  # resumed: the torch optimizers' state continues in the engine
+            self._import_fused_state(tr, models, opts, self.global_step)
+        self.engine_used = "fused"
+        spe = geom.steps_per_epoch
+        total = self.max_steps if self.max_steps > 0 else self.max_epochs * spe
+        logger = CSVLogger(self.root, self.global_rank)
+        self._log_dir = logger.dir
+        model.on_train_start()
+        if self.global_rank == 0:
+            rank_print(0, f"Trainer: fused train-step engine ({tr.comm} comm, {plan['precision']})")
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        last = None
+        try:
+            while self.global_step < total:
+                n = min(tr.cfg.steps_per_launch, total - self.global_step)
+                if self.every_n_train_steps:
+                    n = min(n, self.every_n_train_steps - self.global_step % self.every_n_train_steps)
+                s0 = self.global_step
+                tr.train(n)
+                self.global_step += n
+                rows = tr.losses(s0, self.global_step).tolist()  # one readback per launch
+                for k, row in enumerate(rows):
+                    if (s0 + k + 1) % self.log_every_n_steps == 0:
+                        logger.log(s0 + k + 1, {**dict(zip(names, row)), "train_loss": sum(row)})
+                last = rows[-1]
+                # PL's bookkeeping: the batch that reaches max_steps ends the fit inside its
+                # epoch (epoch e, batch_in_epoch = its index + 1), it does not open the next
+                e, b = divmod(self.global_step - 1, spe)
+                self.current_epoch, self._batch_in_epoch = e, b + 1
+                if self.every_n_train_steps and self.global_step % self.every_n_train_steps == 0:
+                    self._export_fused_state(tr, models, opts)
+                    self._save(model, opts, "last.ckpt")
+            torch.cuda.synchronize(self.device)
+            self.fit_time = time.perf_counter() - t0
+            self.steady_time, self.steady_steps = None, 0
+            if last is not None:
+                self.callback_metrics = {**dict(zip(names, last)), "train_loss": sum(last)}
+        finally:
+            self._export_fused_state(tr, models, opts)
+            tr.close()
+        model.on_train_end()
+        if self.enable_checkpointing:
+            final = f"epoch={max(self.current_epoch - 1, 0) if self._batch_in_epoch == 0 else self.current_epoch}" \
+                    f"-step={self.global_step}.ckpt"
+            self._save(model, opts, final)
+        logger.close()
+        return self
+
+    @staticmethod
+    def _import_fused_state(tr, models, opts, global_step: int) -> None:
+        """A resumed fit: the torch optimizers' restored moments (Adam exp_avg /
+        exp_avg_sq, SGD momentum_buffer) and step count continue in the fused engine
+        (the parameters came in through init_params); ``global_step`` batches ran."""
+        for i, (m, o) in enumerate(zip(models, opts)):
+            st = [o.state.get(p, {}) for p in m.parameters()]
+            keys = ("exp_avg", "exp_avg_sq") if isinstance(o, torch.optim.Adam) else ("momentum_buffer",)
+            for key, dst in zip(keys, (tr.m[i], tr.v[i])):
+                if all(s.get(key) is not None for s in st):
+                    dst.copy_(torch.cat([s[key].reshape(-1).to(dst) for s in st]))
+            steps = [s["step"] for s in st if "step" in s]
+            tr.step_ctr[i] = int(float(steps[0])) if steps else global_step
+        tr.t = global_step
+
+    @staticmethod
+    def _export_fused_state(tr, models, opts) -> None:
+        """Weights back into the modules and the optimizer state into torch format, so
+        checkpoints, hooks and a later module-path fit see the trained state."""
+        tr.synchronize()
+        for i, (m, o) in enumerate(zip(models, opts)):
+            m.load_flat_(tr.model_params(i))
+            step = float(tr.step_ctr[i].item())
+            off = 0
+            for p in m.parameters():
+                n = p.numel()
+                if isinstance(o, torch.optim.Adam):
+                    o.state[p] = {"step": torch.tensor(step), "exp_avg": tr.m[i, off:off + n].view_as(p).clone(),
+                                  "exp_avg_sq": tr.v[i, off:off + n].view_as(p).clone()}
+                elif o.param_groups[0].get("momentum", 0.0):
+                    o.state[p] = {"momentum_buffer": tr.m[i, off:off + n].view_as(p).clone()}
+                off += n
 
     # ------------------------------------------------------------------ checkpoints
     def _ckpt_dir(self) -> Path | None:

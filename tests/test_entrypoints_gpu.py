@@ -99,7 +99,7 @@ def test_demo_layer_split_pipeline_on_gpu(tmp_path):
 def test_demo_lightning_trainer_on_gpu(tmp_path):
     out = _run(["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "100", "--seed", "0", "--no_progress",
                 "--root_dir", str(tmp_path)], finished=False)
-    assert "'global_step': 100" in out, out[-2000:]
+    assert "'global_step': 100" in out and "'engine': 'fused'" in out, out[-2000:]
     ckpts = list(tmp_path.glob("lightning_logs/version_*/checkpoints/*.ckpt"))
     assert ckpts, out[-2000:]
     metrics = list(tmp_path.glob("lightning_logs/version_*/metrics.csv"))
@@ -109,7 +109,8 @@ def test_demo_lightning_trainer_on_gpu(tmp_path):
 def test_lightning_trainer_graph_replay_matches_eager(tmp_path):
     """The Trainer's hipGraph batch replay (two optimizers, toggled params, capturable
     Adam) logs the same losses as its eager batches."""
-    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "64", "--seed", "0", "--no_progress"]
+    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "64", "--seed", "0", "--no_progress",
+            "--engine", "module"]
     g = _summary(_run(base + ["--root_dir", str(tmp_path / "g")], finished=False))
     e = _summary(_run(base + ["--root_dir", str(tmp_path / "e"), "--no_graphs"], finished=False))
     assert g["graph_replays"] >= 50 and e["graph_replays"] == 0, (g, e)
@@ -121,7 +122,8 @@ def test_lightning_trainer_flat_optimizer_matches_torch_adam(tmp_path):
     """The Trainer runs the user's plain torch Adams as the flat-optimizer kernel (one
     launch per optimizer); losses follow torch's own Adam, and the checkpoint carries
     the moments in torch's state format."""
-    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "64", "--seed", "0", "--no_progress"]
+    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "64", "--seed", "0", "--no_progress",
+            "--engine", "module"]
     n = _summary(_run(base + ["--root_dir", str(tmp_path / "n")], finished=False))
     t = _summary(_run(base + ["--root_dir", str(tmp_path / "t"), "--torch_optimizers"], finished=False))
     for k, v in t["metrics"].items():
@@ -132,6 +134,54 @@ def test_lightning_trainer_flat_optimizer_matches_torch_adam(tmp_path):
     st = ck["optimizer_states"][0]["state"]
     assert len(st) == 10 and all("exp_avg" in s and "exp_avg_sq" in s for s in st.values())
     assert all(float(s["step"]) == 64 for s in st.values())
+
+
+def _ckpt_state(path):
+    import torch
+
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def test_lightning_trainer_fused_engine_matches_module_path(tmp_path):
+    """Trainer(engine='auto') runs LitToyModel on the fused train-step engine (its
+    fused_spec); the trained weights and the Adam moments it exports into the torch
+    optimizers match the per-batch module path (hipGraph replays, flat Adam kernel) to
+    fp32 summation-order tolerance, and global_step / epoch bookkeeping agree."""
+    import torch
+
+    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--steps", "96", "--seed", "0", "--no_progress"]
+    f = _summary(_run(base + ["--root_dir", str(tmp_path / "f")], finished=False))
+    m = _summary(_run(base + ["--root_dir", str(tmp_path / "m"), "--engine", "module"], finished=False))
+    assert f["engine"] == "fused" and m["engine"] == "module" and f["global_step"] == m["global_step"] == 96
+    cf, cm = _ckpt_state(f["checkpoint"]), _ckpt_state(m["checkpoint"])
+    assert cf["epoch"] == cm["epoch"] and cf["batch_in_epoch"] == cm["batch_in_epoch"]
+    for k, v in cm["state_dict"].items():
+        torch.testing.assert_close(cf["state_dict"][k], v, rtol=0, atol=2e-4)
+    for of, om in zip(cf["optimizer_states"], cm["optimizer_states"]):
+        for i, s in om["state"].items():
+            assert float(of["state"][i]["step"]) == float(s["step"]) == 96
+            torch.testing.assert_close(of["state"][i]["exp_avg"], s["exp_avg"], rtol=1e-3, atol=1e-5)
+            torch.testing.assert_close(of["state"][i]["exp_avg_sq"], s["exp_avg_sq"], rtol=1e-3, atol=1e-7)
+    # the fused engine logs each model's loss every log_every_n_steps like the module path
+    for d in ("f", "m"):
+        rows = list((tmp_path / d).glob("lightning_logs/version_*/metrics.csv"))[0].read_text().splitlines()
+        assert "loss/lossX" in rows[0] and len(rows) > 2, rows[:3]
+
+
+def test_lightning_trainer_fused_engine_resume_is_bit_exact(tmp_path):
+    """A fused-engine fit stopped at step 32 (last.ckpt: weights + torch-format Adam
+    state) and resumed to 64 ends bit-identical to an uninterrupted 64-step fit."""
+    import torch
+
+    base = ["demo_pytorch_lightning.py", "--gpus", "1", "--seed", "0", "--no_progress"]
+    full = _summary(_run(base + ["--steps", "64", "--root_dir", str(tmp_path / "a")], finished=False))
+    _run(base + ["--steps", "32", "--every_n_train_steps", "32", "--root_dir", str(tmp_path / "b")], finished=False)
+    res = _summary(_run(base + ["--steps", "64", "--ckpt_path", "last", "--root_dir", str(tmp_path / "b")],
+                        finished=False))
+    assert full["engine"] == res["engine"] == "fused" and res["global_step"] == 64
+    ca, cb = _ckpt_state(full["checkpoint"]), _ckpt_state(res["checkpoint"])
+    for k, v in ca["state_dict"].items():
+        assert torch.equal(cb["state_dict"][k], v), k
 
 
 def test_demo_layer_split_fused_engine_on_gpu(tmp_path):
