@@ -100,9 +100,11 @@ def test_demo_bf16_end_to_end(tmp_path):
     assert all(0.0 < v < 4.0 for v in s["final_loss"]), s
 
 
-def test_trainer_precision_bf16(tmp_path):
+@pytest.mark.parametrize("engine", ["auto", "module"])
+def test_trainer_precision_bf16(tmp_path, engine):
     r = subprocess.run([sys.executable, "demo_pytorch_lightning.py", "--gpus", "1", "--steps", "40", "--seed", "0",
-                        "--no_progress", "--precision", "bf16", "--root_dir", str(tmp_path)], cwd=ROOT,
-                       capture_output=True, text=True, timeout=120)
+                        "--no_progress", "--precision", "bf16", "--root_dir", str(tmp_path), "--engine", engine],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "'global_step': 40" in r.stdout
+    assert f"'engine': '{'fused' if engine == 'auto' else 'module'}'" in r.stdout, r.stdout[-1500:]

@@ -62,7 +62,7 @@ def test_module_step_graph_equals_eager_on_xgmi():
     assert torch.equal(g[0][0], g[1][0]), "replicas diverged"
 
 
-def _trainer_rank(rank, world, graphs, root):
+def _trainer_rank(rank, world, graphs, root, engine="module"):
     os.environ["LOCAL_RANK"] = "0"  # both ranks on the one GPU (the process group is already up)
     sys.path.insert(0, ROOT)
     from demo_pytorch_lightning import LitToyModel
@@ -74,10 +74,10 @@ def _trainer_rank(rank, world, graphs, root):
     model = LitToyModel()
     tr = Trainer(gpus=2, max_steps=12, accelerator="gpu", strategy="ddp", log_every_n_steps=4,
                  default_root_dir=os.path.join(root, f"g{int(graphs)}"), enable_progress_bar=False,
-                 use_graphs=graphs, enable_checkpointing=False)
+                 use_graphs=graphs, enable_checkpointing=False, engine=engine)
     tr.fit(model, dl)
     return {k: v.cpu() for k, v in model.state_dict().items()}, tr.graph_replays, \
-        getattr(getattr(tr, "_stepper", None), "fallback_reason", None)
+        getattr(getattr(tr, "_stepper", None), "fallback_reason", None), tr.engine_used
 
 
 def test_trainer_graph_equals_eager_on_xgmi(tmp_path):
@@ -86,12 +86,27 @@ def test_trainer_graph_equals_eager_on_xgmi(tmp_path):
     g = run_ranks(_trainer_rank, 2, (True, str(tmp_path)), timeout=300)
     e = run_ranks(_trainer_rank, 2, (False, str(tmp_path)), timeout=300)
     for r in range(2):
-        sd, replays, why = g[r]
+        sd, replays, why, _ = g[r]
         assert replays > 0, why
         for k in sd:
             assert torch.equal(sd[k], e[r][0][k]), k
     for k in g[0][0]:
         assert torch.equal(g[0][0][k], g[1][0][k]), k
+
+
+def test_trainer_fused_engine_on_two_ranks(tmp_path):
+    """Trainer(engine='auto') with DDP on two ranks runs LitToyModel on the fused
+    train-step engine (in-kernel xGMI gradient exchange, DistributedSampler order) and
+    ends where the per-batch module path ends, to fp32 summation-order tolerance, with
+    identical replicas."""
+    f = run_ranks(_trainer_rank, 2, (False, str(tmp_path / "f"), "auto"), timeout=300)
+    e = run_ranks(_trainer_rank, 2, (False, str(tmp_path / "e"), "module"), timeout=300)
+    for r in range(2):
+        assert f[r][3] == "fused" and e[r][3] == "module", (f[r][3], e[r][3])
+        for k, v in e[r][0].items():
+            torch.testing.assert_close(f[r][0][k], v, rtol=0, atol=1e-4)
+    for k in f[0][0]:
+        assert torch.equal(f[0][0][k], f[1][0][k]), k
 
 
 def _full_cap_rank(rank, world, calls, graph_reps):
