@@ -87,3 +87,33 @@ def test_gemm_backend_knob():
     # on CPU tensors every backend runs the PyTorch reference
     a, b = torch.randn(64, 32).bfloat16(), torch.randn(48, 32).bfloat16()
     torch.testing.assert_close(g.gemm(a, b, out_dtype=torch.float32), a.float() @ b.float().t())
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb,splits", [
+    (2048, 2048, 8192, True, True, 4),     # dW of a 2048-wide layer, batch 8192: 64 tiles x 4 slices
+    (1024, 1024, 16384, True, True, 16),   # dW of a 1024-wide layer, batch 16384: 16 tiles x 16
+    (520, 264, 2048, True, True, 4),       # ragged: 6 tiles, 32 K-tiles -> 4 slices of 8
+    (4096, 4096, 8192, True, True, 0),     # 256 tiles fill the chip: no split
+    (2048, 2048, 8192 + 64, True, True, 0),  # odd K-tile count: no even slices
+    (2048, 2048, 512, True, True, 0),      # 8 K-tiles: slices would drop below 8
+])
+def test_ph8_split_k_plan(M, N, K, ta, tb, splits):
+    """The 8-phase GEMM's split-K plan (host code in libdtp.so, no GPU needed): slices
+    only for problems with < 128 256x256 tiles, tiles x slices <= 256, every slice an
+    even number (>= 8) of 64-deep K-tiles; the workspace holds one f32 plane per slice."""
+    from distributed_training_pytorch_amd import _native as nat
+
+    try:
+        lib = nat.load()
+    except nat.NativeUnavailable as e:
+        pytest.skip(f"native library not built: {e}")
+    a = nat.GemmArgs()
+    a.A, a.B = 256, 256  # 16-byte aligned addresses; nothing is dereferenced
+    a.M, a.N, a.K = M, N, K
+    a.lda = M if ta else K
+    a.ldb = N if tb else K
+    a.dtype, a.out_dtype, a.trans_a, a.trans_b = nat.DT_BF16, nat.DT_F32, int(ta), int(tb)
+    a.splitk = 0
+    assert lib.dtp_gemm_workspace(a) == 4 * splits * M * N
+    a.out_dtype = nat.DT_BF16  # a bf16 output (or an activation epilogue) never splits
+    assert lib.dtp_gemm_workspace(a) == 0
