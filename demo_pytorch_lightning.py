@@ -110,7 +110,9 @@ def main(argv=None):
         sps = None
         if getattr(trainer, "fit_time", None):
             sps = trainer.global_step * a.batch_size * getattr(trainer, "world_size", 1) / trainer.fit_time
-        steady = None  # after the first 10 batches (eager warm-up, graph capture, first kernel loads)
+        # steady state: module path after the first 10 batches (eager warm-up, graph capture,
+        # first kernel loads); fused engine after its first launch
+        steady = None
         if getattr(trainer, "steady_time", None):
             steady = trainer.steady_steps * a.batch_size * getattr(trainer, "world_size", 1) / trainer.steady_time
         print(f"[Process 0] summary: {{'global_step': {trainer.global_step}, 'metrics': {trainer.callback_metrics}, "

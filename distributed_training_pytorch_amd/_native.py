@@ -163,6 +163,7 @@ class OptArgs(ctypes.Structure):
         ("loss_scale", c_float),
         ("pad_", c_int),
         ("hp", Hyper),
+        ("shadow", c_void_p),
     ]
 
 

@@ -142,6 +142,7 @@ struct DtpOptArgs {
   float loss_scale;   // applied to the all-reduced losses (1/world)
   int pad_;
   DtpHyper hp;
+  void* shadow;       // [n_models][P] bf16 copy of the updated params, or null
 };
 
 int dtp_flat_optimizer(const DtpOptArgs* a, void* stream);

@@ -2,13 +2,18 @@
 // gradient all-reduce: one launch updates every model (the reference runs
 // ~7 elementwise kernels per parameter tensor x 10 tensors x 2 models,
 // SURVEY.md §2.6 K11).  The DDP 1/W averaging and the loss bookkeeping are
-// fused in.
+// fused in, and so is the bf16 compute copy of the weights (`shadow`): the
+// bf16-compute GEMM path reads its weight operands from it instead of casting the
+// fp32 masters before every forward (2 B/parameter written here vs a 6 B/parameter
+// cast pass and one launch per weight tensor).
 #include <string>
 
 #include "dtp_api.h"
 #include "optim_core.h"
 
 namespace dtp {
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
   const int model = blockIdx.y;
@@ -17,9 +22,11 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
   float* m = a.opt_m + (size_t)model * a.P;
   float* v = a.opt_v ? a.opt_v + (size_t)model * a.P : nullptr;
   const float* g = a.grad + (size_t)model * a.P;
+  __bf16* sh = a.shadow ? reinterpret_cast<__bf16*>(a.shadow) + (size_t)model * a.P : nullptr;
   // rows of 16-byte aligned float4s when every model row is (P % 4 == 0): 4 elements
   // per thread and load (the update is HBM-bound: 28 B per parameter)
-  const bool vec = (a.P & 3) == 0 && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)g | (uintptr_t)(v ? v : p)) & 15) == 0;
+  const bool vec = (a.P & 3) == 0 && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)g | (uintptr_t)(v ? v : p)) & 15) == 0 &&
+                   ((uintptr_t)sh & 7) == 0;
   if (a.kind == DTP_MODE_ADAM && vec) {
     const AdamScalars s = adam_scalars(a.hp, t + 1);
     const int P4 = a.P >> 2;
@@ -34,6 +41,7 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
       reinterpret_cast<float4*>(p)[i] = w;
       reinterpret_cast<float4*>(m)[i] = mi;
       reinterpret_cast<float4*>(v)[i] = vi;
+      if (sh) reinterpret_cast<bf16x4*>(sh)[i] = bf16x4{(__bf16)w.x, (__bf16)w.y, (__bf16)w.z, (__bf16)w.w};
     }
   } else if (a.kind == DTP_MODE_ADAM) {
     const AdamScalars s = adam_scalars(a.hp, t + 1);
@@ -43,6 +51,7 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
       p[i] = w;
       m[i] = mi;
       v[i] = vi;
+      if (sh) sh[i] = (__bf16)w;
     }
   } else {
     const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
@@ -51,6 +60,7 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
       sgd_update(w, bi, g[i] * a.hp.grad_scale, lr, mom, wd, t == 0);
       p[i] = w;
       m[i] = bi;
+      if (sh) sh[i] = (__bf16)w;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -13,7 +13,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.gemm import mark_fused_grad
+from ..ops.gemm import ComputeShadow, mark_fused_grad
 from .toy import ToyModel
 
 
@@ -46,6 +46,18 @@ class ModelBank(nn.Module):
             m._flat = flat[i]
         self.flat = flat
         self.flat_grad = grad
+        if getattr(self, "_shadow", None) is not None:  # the old shadow's views point at the old buffer
+            self._shadow.detach_()
+            self._shadow = None
+
+    def compute_shadow(self):
+        """A bf16 ``ComputeShadow`` of the bank's weight matrices (the GEMM path's
+        operands), for ``FlatOptimizer(..., shadow=bank.compute_shadow())``.  Rebuilt
+        after ``.to()`` / ``rebind()``."""
+        if getattr(self, "_shadow", None) is None:
+            weights = [p for m in self.models for n, p in m.layers.named_parameters() if n.endswith("weight")]
+            self._shadow = ComputeShadow(self.flat, weights)
+        return self._shadow
 
     def _apply(self, fn, recurse=True):
         out = super()._apply(fn, recurse)

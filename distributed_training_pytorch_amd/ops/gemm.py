@@ -289,6 +289,64 @@ def _grad_ready(p: torch.Tensor) -> None:
         fn(p)
 
 
+class ComputeShadow:
+    """A bf16 copy of a flat fp32 parameter buffer, for the bf16-compute GEMM path.
+
+    ``MLPFunction`` casts every fp32 master weight to bf16 before each forward: one
+    launch and 6 B of traffic per parameter.  With a shadow attached, the optimizer
+    kernel writes the rounded weights in the same pass as the update (2 B per
+    parameter, ``flat_optimizer_step(shadow=...)``) and the forward reads its operands
+    from the shadow's views.  The copy is bit-identical to ``w.to(torch.bfloat16)``
+    (both round to nearest even).
+
+    Staleness: the shadow is trusted only while the version counters of the flat
+    buffer and of every attached parameter are the ones recorded when it was last
+    written.  Any torch in-place write (``load_state_dict``, ``copy_``, a broadcast)
+    bumps one of them, and the next forward re-casts the whole buffer once.  The
+    native optimizer writes through raw pointers (no version bump) and calls
+    ``mark_fresh`` after it has written both."""
+
+    def __init__(self, flat: torch.Tensor, params, dtype: torch.dtype = torch.bfloat16):
+        if dtype != torch.bfloat16 or flat.dtype != torch.float32 or not flat.is_contiguous():
+            raise ValueError("ComputeShadow: a contiguous fp32 flat buffer and a bf16 shadow")
+        self.flat, self.params = flat, list(params)
+        self.buf = torch.empty_like(flat, dtype=dtype)
+        base, es, n = flat.data_ptr(), flat.element_size(), flat.numel()
+        whole = self.buf.view(-1)
+        for p in self.params:
+            off = (p.data_ptr() - base) // es
+            if p.dtype != flat.dtype or not p.is_contiguous() or off < 0 or off + p.numel() > n:
+                raise ValueError("ComputeShadow: every parameter must be a contiguous view of the flat buffer")
+            p._dtp_shadow = (self, whole[off:off + p.numel()].view_as(p))
+        self._token = None
+
+    def _current(self):
+        return (self.flat._version, *(p._version for p in self.params))
+
+    def view(self, p: torch.Tensor) -> torch.Tensor:
+        """The bf16 operand for parameter ``p``, re-cast first if the masters changed."""
+        if self._token != self._current():
+            with torch.no_grad():
+                self.buf.copy_(self.flat)
+            self._token = self._current()
+        return p._dtp_shadow[1]
+
+    def mark_fresh(self) -> None:
+        self._token = self._current()
+
+    def detach_(self) -> None:
+        for p in self.params:
+            if getattr(p, "_dtp_shadow", (None,))[0] is self:
+                del p._dtp_shadow
+
+
+def _compute_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    sh = getattr(w, "_dtp_shadow", None)
+    if sh is not None and sh[0].buf.dtype == dtype:
+        return sh[0].view(w)
+    return w.detach().to(dtype).contiguous()
+
+
 class MLPFunction(torch.autograd.Function):
     """y = L_{n-1}(... LeakyReLU(L_0(x)) ...) with every matmul through ``gemm``.
 
@@ -301,7 +359,7 @@ class MLPFunction(torch.autograd.Function):
     def forward(ctx, x, slope, compute_dtype, *params):
         weights, biases = params[0::2], params[1::2]
         L = len(weights)
-        ws = [w.detach().to(compute_dtype).contiguous() for w in weights]
+        ws = [_compute_weight(w, compute_dtype) for w in weights]
         h = x.detach().to(compute_dtype).contiguous()
         hs = [h]
         for l in range(L):

@@ -70,18 +70,22 @@ def sgd_update_ref(p: torch.Tensor, buf: torch.Tensor, g: torch.Tensor, first: b
 
 
 def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: float = 1.0,
-                        loss_log=None, loss_scale: float = 1.0, slope: float = 0.01) -> None:
+                        loss_log=None, loss_scale: float = 1.0, slope: float = 0.01, shadow=None) -> None:
     """One optimizer step over [n_models, P] flat buffers.
 
     ``grad`` is [n_models*P (+ n_models losses)] -- the all-reduced comm buffer;
-    ``step`` is the per-model int32 step counter (device or CPU).
+    ``step`` is the per-model int32 step counter (device or CPU); ``shadow`` (optional,
+    bf16 [n_models, P]) receives the updated parameters rounded to bf16 in the same pass.
     """
     n_models, P = params.shape
+    if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.shape != params.shape
+                               or not shadow.is_contiguous() or shadow.device != params.device):
+        raise ValueError("flat_optimizer_step: shadow must be a contiguous bf16 tensor shaped like params")
     if params.is_cuda and nat.native_enabled():
         lib = nat.require(params.device)
         a = nat.OptArgs(nat.ptr(params), nat.ptr(m), nat.ptr(v), nat.ptr(step), nat.ptr(grad),
                         nat.ptr(loss_log), 0 if loss_log is None else loss_log.shape[0], n_models, P, cfg.kind,
-                        loss_scale, 0, cfg.hyper(slope, grad_scale))
+                        loss_scale, 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow))
         nat.check(lib.dtp_flat_optimizer(ctypes.byref(a), nat.stream_ptr()), "dtp_flat_optimizer")
         return
     g = grad[: n_models * P].view(n_models, P) * grad_scale
@@ -94,6 +98,8 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
         if loss_log is not None:
             loss_log[t % loss_log.shape[0], i] = grad[n_models * P + i] * loss_scale
         step[i] = t + 1
+    if shadow is not None:
+        shadow.copy_(params)
 
 
 class FlatOptimizer:
@@ -101,7 +107,12 @@ class FlatOptimizer:
     (replaces the reference's two torch.optim.Adam, each ~7 kernels x 10 tensors)."""
 
     def __init__(self, flat_params: torch.Tensor, flat_grad: torch.Tensor, cfg: OptimConfig | None = None,
-                 slope: float = 0.01):
+                 slope: float = 0.01, shadow=None):
+        """``shadow``: an ``ops.gemm.ComputeShadow`` of ``flat_params``; every step also
+        writes its bf16 copy (the bf16-compute forward then needs no weight casts)."""
+        self.shadow = shadow
+        if shadow is not None and shadow.flat.data_ptr() != flat_params.data_ptr():
+            raise ValueError("FlatOptimizer: the shadow must be of flat_params")
         self.params = flat_params if flat_params.dim() == 2 else flat_params.view(1, -1)
         self.grad = flat_grad if flat_grad.dim() == 2 else flat_grad.view(1, -1)
         self.cfg = cfg or OptimConfig()
@@ -123,7 +134,12 @@ class FlatOptimizer:
         else:
             self._buf[: n * P].copy_(self.grad.reshape(-1))
             buf = self._buf
-        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.cfg, slope=self.slope)
+        sh = self.shadow
+        fresh = sh is not None and sh._token == sh._current()  # else the next forward re-casts anyway
+        flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.cfg, slope=self.slope,
+                            shadow=sh.buf.view(self.params.shape) if fresh else None)
+        if fresh:
+            sh.mark_fresh()
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         self.grad.zero_()

@@ -62,6 +62,16 @@ class CSVLogger:
             self._w.writeheader()
         self._w.writerow(row)
 
+    def log_rows(self, steps, names, rows):
+        """One row per (step, values): ``names[i]`` = ``values[i]`` plus their sum as
+        ``train_loss`` (the fused engine's per-launch loss block, written in one call)."""
+        if self.dir is None or not steps:
+            return
+        if self._w is None:
+            self.log(steps[0], {**dict(zip(names, rows[0])), "train_loss": sum(rows[0])})
+            steps, rows = steps[1:], rows[1:]
+        self._w.writerows({"step": s, **dict(zip(names, r)), "train_loss": sum(r)} for s, r in zip(steps, rows))
+
     def flush(self):
         if self.dir is not None:
             self._f.flush()
@@ -459,6 +469,10 @@ class Trainer:
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
         last = None
+        # steady-state clock: from the end of the first launch on (engine set-up, first
+        # kernel loads and the prologue of a fresh launch excluded); every launch ends in
+        # a loss readback, so the clock starts and stops on a synchronised device
+        steady_t0, steady_from = None, None
         try:
             while self.global_step < total:
                 n = min(tr.cfg.steps_per_launch, total - self.global_step)
@@ -468,10 +482,12 @@ class Trainer:
                 tr.train(n)
                 self.global_step += n
                 rows = tr.losses(s0, self.global_step).tolist()  # one readback per launch
-                for k, row in enumerate(rows):
-                    if (s0 + k + 1) % self.log_every_n_steps == 0:
-                        logger.log(s0 + k + 1, {**dict(zip(names, row)), "train_loss": sum(row)})
+                every = self.log_every_n_steps
+                first = -(s0 + 1) % every  # index of the first logged step of this launch
+                logger.log_rows(list(range(s0 + first + 1, self.global_step + 1, every)), names, rows[first::every])
                 last = rows[-1]
+                if steady_t0 is None:
+                    steady_t0, steady_from = time.perf_counter(), self.global_step
                 # PL's bookkeeping: the batch that reaches max_steps ends the fit inside its
                 # epoch (epoch e, batch_in_epoch = its index + 1), it does not open the next
                 e, b = divmod(self.global_step - 1, spe)
@@ -480,8 +496,11 @@ class Trainer:
                     self._export_fused_state(tr, models, opts)
                     self._save(model, opts, "last.ckpt")
             torch.cuda.synchronize(self.device)
-            self.fit_time = time.perf_counter() - t0
+            t1 = time.perf_counter()
+            self.fit_time = t1 - t0
             self.steady_time, self.steady_steps = None, 0
+            if steady_t0 is not None and self.global_step > steady_from:
+                self.steady_time, self.steady_steps = t1 - steady_t0, self.global_step - steady_from
             if last is not None:
                 self.callback_metrics = {**dict(zip(names, last)), "train_loss": sum(last)}
         finally:

@@ -1,11 +1,11 @@
 #!/bin/bash
 # round-3 end-of-session validation: GPU suite, smoke, driver-style bench lines, kernel trace of the K=20 call
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r3z
+mkdir -p gpurun_out/r3y
 bash scripts/gpu_steps.sh \
-  "900|r3z/gpu_suite|python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests" \
-  "180|r3z/smoke|python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
-  "180|r3z/bench_k20|for i in 1 2 3; do python bench.py --steps 20 --warmup 5; done" \
-  "180|r3z/bench_default|python bench.py" \
-  "180|r3z/bench_bf16|python bench.py --precision bf16" \
-  "200|r3z/rocprof_k20|timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3z/prof -o k20 -- python3 bench.py --steps 20 --warmup 5"
+  "900|r3y/gpu_suite|python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests" \
+  "180|r3y/smoke|python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
+  "180|r3y/bench_k20|for i in 1 2 3; do python bench.py --steps 20 --warmup 5; done" \
+  "180|r3y/bench_default|python bench.py" \
+  "180|r3y/bench_bf16|python bench.py --precision bf16" \
+  "200|r3y/rocprof_k20|timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3y/prof -o k20 -- python3 bench.py --steps 20 --warmup 5"

@@ -205,3 +205,23 @@ def test_trainer_metric_rows_cover_every_logged_step(tmp_path):
     assert keys and set(keys) == set(tr.callback_metrics)
     assert all(float(rows[-1][k]) == tr.callback_metrics[k] for k in keys)
     assert len({rows[i][keys[0]] for i in range(steps)}) > steps // 2  # per-step values, not one repeated
+
+
+def test_csv_logger_block_rows_match_single_rows(tmp_path):
+    """CSVLogger.log_rows (the fused engine's one call per launch) writes the same
+    file as one log() per step: header order, step column, per-name values, sum."""
+    from distributed_training_pytorch_amd.trainer.trainer import CSVLogger
+
+    names = ["loss/lossX", "loss/lossY"]
+    rows = [[0.5 + k, 0.25 * k] for k in range(5)]
+    steps = [4, 8, 12, 16, 20]
+    a = CSVLogger(str(tmp_path / "a"), 0)
+    for s, r in zip(steps, rows):
+        a.log(s, {**dict(zip(names, r)), "train_loss": sum(r)})
+    a.close()
+    b = CSVLogger(str(tmp_path / "b"), 0)
+    b.log_rows(steps[:2], names, rows[:2])
+    b.log_rows([], names, [])
+    b.log_rows(steps[2:], names, rows[2:])
+    b.close()
+    assert (a.dir / "metrics.csv").read_text() == (b.dir / "metrics.csv").read_text()

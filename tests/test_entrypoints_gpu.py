@@ -162,10 +162,19 @@ def test_lightning_trainer_fused_engine_matches_module_path(tmp_path):
             assert float(of["state"][i]["step"]) == float(s["step"]) == 96
             torch.testing.assert_close(of["state"][i]["exp_avg"], s["exp_avg"], rtol=1e-3, atol=1e-5)
             torch.testing.assert_close(of["state"][i]["exp_avg_sq"], s["exp_avg_sq"], rtol=1e-3, atol=1e-7)
-    # the fused engine logs each model's loss every log_every_n_steps like the module path
+    # the fused engine logs each model's loss at the same steps as the module path
+    import csv
+
+    logs = {}
     for d in ("f", "m"):
-        rows = list((tmp_path / d).glob("lightning_logs/version_*/metrics.csv"))[0].read_text().splitlines()
-        assert "loss/lossX" in rows[0] and len(rows) > 2, rows[:3]
+        path = list((tmp_path / d).glob("lightning_logs/version_*/metrics.csv"))[0]
+        logs[d] = list(csv.DictReader(open(path)))
+        assert "loss/lossX" in logs[d][0] and len(logs[d]) > 2, logs[d][:3]
+    assert [r["step"] for r in logs["f"]] == [r["step"] for r in logs["m"]]
+    for rf, rm in zip(logs["f"], logs["m"]):
+        for k in ("loss/lossX", "loss/lossY"):
+            assert abs(float(rf[k]) - float(rm[k])) <= 1e-4 * max(1.0, abs(float(rm[k]))), (rf, rm)
+    assert f["steady_samples_per_s"] is not None and f["steady_samples_per_s"] > 0
 
 
 def test_lightning_trainer_fused_engine_resume_is_bit_exact(tmp_path):

@@ -117,3 +117,45 @@ def test_ph8_split_k_plan(M, N, K, ta, tb, splits):
     assert lib.dtp_gemm_workspace(a) == 4 * splits * M * N
     a.out_dtype = nat.DT_BF16  # a bf16 output (or an activation epilogue) never splits
     assert lib.dtp_gemm_workspace(a) == 0
+
+
+def test_compute_shadow_tracks_the_masters():
+    """ComputeShadow: the bf16 operands equal w.to(bf16) after every optimizer step
+    (the optimizer writes them in its own pass and marks them fresh), and any torch
+    in-place write to the masters (an edit, load_state_dict) is detected by the
+    version counters and re-cast before the next use."""
+    from distributed_training_pytorch_amd.models.bank import ModelBank
+    from distributed_training_pytorch_amd.ops.gemm import _compute_weight
+    from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig
+
+    torch.manual_seed(0)
+    bank = ModelBank(2, hidden=32, depth=2, compute_dtype=torch.bfloat16)
+    sh = bank.compute_shadow()
+    opt = FlatOptimizer(bank.flat, bank.flat_grad, OptimConfig(lr=1e-2), shadow=sh)
+    weights = [p for m in bank.models for n, p in m.layers.named_parameters() if n.endswith("weight")]
+
+    def check():
+        for w in weights:
+            v = _compute_weight(w, torch.bfloat16)
+            assert v.dtype == torch.bfloat16 and torch.equal(v, w.detach().to(torch.bfloat16))
+
+    check()
+    for _ in range(3):
+        bank.flat_grad.normal_()
+        opt.step()
+        assert sh._token == sh._current()  # written by the step itself, no re-cast pending
+        check()
+    with torch.no_grad():
+        weights[3].mul_(2.0)
+    assert sh._token != sh._current()
+    check()
+    bank[0].load_state_dict({k: torch.ones_like(t) for k, t in bank[0].state_dict().items()})
+    check()
+    assert float(_compute_weight(weights[0], torch.bfloat16).float().mean()) == 1.0
+    # a rebuilt bank (``.to()`` re-packs the buffers) drops the old shadow's views
+    bank = bank.to(torch.float32)
+    assert getattr(bank, "_shadow", None) is None
+    assert not hasattr(bank[0].layers[0].weight, "_dtp_shadow")
+    # fp32 compute never uses it
+    w = bank[0].layers[0].weight
+    assert _compute_weight(w, torch.float32).dtype == torch.float32

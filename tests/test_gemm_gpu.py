@@ -315,3 +315,32 @@ def test_gemm_bf16_ph8_split_k(ta, tb, shape):
     torch.testing.assert_close(c, old + 0.5 * ref + bias, rtol=1e-4, atol=2e-3 * K ** 0.5)
     c2 = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
     torch.testing.assert_close(c2, ref, rtol=1e-4, atol=2e-3 * K ** 0.5)
+
+
+def test_compute_shadow_training_is_bit_identical():
+    """bf16-compute wide ModelBank: Adam writing the bf16 weight copy in its own pass
+    (ComputeShadow) trains bit-identically to casting the fp32 masters before every
+    forward, and the shadow equals w.to(bf16) after each step."""
+    from distributed_training_pytorch_amd.models.bank import ModelBank
+    from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig
+
+    def run(shadow):
+        torch.manual_seed(0)
+        bank = ModelBank(2, hidden=256, depth=2, compute_dtype=torch.bfloat16).to(DEV)
+        sh = bank.compute_shadow() if shadow else None
+        opt = FlatOptimizer(bank.flat, bank.flat_grad, OptimConfig(lr=1e-3), shadow=sh)
+        g = torch.Generator().manual_seed(1)
+        for _ in range(4):
+            x = torch.randn(512, 2, generator=g).to(DEV)
+            y = torch.randn(512, 1, generator=g).to(DEV)
+            bank.zero_grad()
+            sum(torch.nn.functional.mse_loss(o, y) for o in bank(x)).backward()
+            opt.step()
+            if sh is not None:
+                assert torch.equal(sh.buf, bank.flat.to(torch.bfloat16))
+        return bank.flat.clone(), sh
+
+    a, _ = run(False)
+    b, sh = run(True)
+    assert sh._token == sh._current()
+    assert torch.equal(a, b)
