@@ -111,7 +111,7 @@ def main(argv=None):
         if getattr(trainer, "fit_time", None):
             sps = trainer.global_step * a.batch_size * getattr(trainer, "world_size", 1) / trainer.fit_time
         # steady state: module path after the first 10 batches (eager warm-up, graph capture,
-        # first kernel loads); fused engine after its first launch
+        # first kernel loads); fused engine after its first launch of 10 steps
         steady = None
         if getattr(trainer, "steady_time", None):
             steady = trainer.steady_steps * a.batch_size * getattr(trainer, "world_size", 1) / trainer.steady_time

@@ -164,6 +164,7 @@ class OptArgs(ctypes.Structure):
         ("pad_", c_int),
         ("hp", Hyper),
         ("shadow", c_void_p),
+        ("shadow_ld", c_longlong),
     ]
 
 

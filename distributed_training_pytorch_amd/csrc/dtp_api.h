@@ -142,7 +142,8 @@ struct DtpOptArgs {
   float loss_scale;   // applied to the all-reduced losses (1/world)
   int pad_;
   DtpHyper hp;
-  void* shadow;       // [n_models][P] bf16 copy of the updated params, or null
+  void* shadow;       // [n_models][shadow_ld] bf16 copy of the updated params, or null
+  long long shadow_ld;  // row stride of shadow in elements (>= P)
 };
 
 int dtp_flat_optimizer(const DtpOptArgs* a, void* stream);

@@ -13,6 +13,7 @@
 
 namespace dtp {
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
@@ -22,7 +23,7 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
   float* m = a.opt_m + (size_t)model * a.P;
   float* v = a.opt_v ? a.opt_v + (size_t)model * a.P : nullptr;
   const float* g = a.grad + (size_t)model * a.P;
-  __bf16* sh = a.shadow ? reinterpret_cast<__bf16*>(a.shadow) + (size_t)model * a.P : nullptr;
+  __bf16* sh = a.shadow ? reinterpret_cast<__bf16*>(a.shadow) + (size_t)model * a.shadow_ld : nullptr;
   // rows of 16-byte aligned float4s when every model row is (P % 4 == 0): 4 elements
   // per thread and load (the update is HBM-bound: 28 B per parameter)
   const bool vec = (a.P & 3) == 0 && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)g | (uintptr_t)(v ? v : p)) & 15) == 0 &&
@@ -43,6 +44,34 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
       reinterpret_cast<float4*>(v)[i] = vi;
       if (sh) reinterpret_cast<bf16x4*>(sh)[i] = bf16x4{(__bf16)w.x, (__bf16)w.y, (__bf16)w.z, (__bf16)w.w};
     }
+  } else if (a.kind == DTP_MODE_ADAM && sh) {
+    // unaligned rows (odd P: every bias-terminated MLP) with a shadow: two elements per
+    // thread, so the shadow is written as one 4-byte bf16 pair per lane (the shadow's
+    // rows are 512-byte aligned, ComputeShadow); single 2-byte stores per lane ran the
+    // whole kernel 15 % slower
+    const AdamScalars s = adam_scalars(a.hp, t + 1);
+    const int P2 = (a.P + 1) >> 1;
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < P2; j += gridDim.x * kBlock) {
+      const int i = 2 * j;
+      const bool two = i + 1 < a.P;
+      float w0 = p[i], m0 = m[i], v0 = v[i];
+      const float g0 = g[i];
+      float w1 = 0.f, m1 = 0.f, v1 = 0.f, g1 = 0.f;
+      if (two) w1 = p[i + 1], m1 = m[i + 1], v1 = v[i + 1], g1 = g[i + 1];
+      adam_update(w0, m0, v0, g0 * a.hp.grad_scale, s);
+      p[i] = w0;
+      m[i] = m0;
+      v[i] = v0;
+      if (two) {
+        adam_update(w1, m1, v1, g1 * a.hp.grad_scale, s);
+        p[i + 1] = w1;
+        m[i + 1] = m1;
+        v[i + 1] = v1;
+        *reinterpret_cast<bf16x2*>(sh + i) = bf16x2{(__bf16)w0, (__bf16)w1};
+      } else {
+        sh[i] = (__bf16)w0;
+      }
+    }
   } else if (a.kind == DTP_MODE_ADAM) {
     const AdamScalars s = adam_scalars(a.hp, t + 1);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.P; i += gridDim.x * kBlock) {
@@ -51,7 +80,6 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
       p[i] = w;
       m[i] = mi;
       v[i] = vi;
-      if (sh) sh[i] = (__bf16)w;
     }
   } else {
     const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;

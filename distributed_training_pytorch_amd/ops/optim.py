@@ -75,17 +75,19 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
 
     ``grad`` is [n_models*P (+ n_models losses)] -- the all-reduced comm buffer;
     ``step`` is the per-model int32 step counter (device or CPU); ``shadow`` (optional,
-    bf16 [n_models, P]) receives the updated parameters rounded to bf16 in the same pass.
+    bf16 [n_models, >= P], unit column stride) receives the updated parameters rounded
+    to bf16 in the same pass, row i at ``shadow[i, :P]``.
     """
     n_models, P = params.shape
-    if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.shape != params.shape
-                               or not shadow.is_contiguous() or shadow.device != params.device):
-        raise ValueError("flat_optimizer_step: shadow must be a contiguous bf16 tensor shaped like params")
+    if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.dim() != 2 or shadow.shape[0] != n_models
+                               or shadow.shape[1] < P or shadow.stride(1) != 1 or shadow.device != params.device):
+        raise ValueError("flat_optimizer_step: shadow must be a bf16 [n_models, >= P] tensor with unit column stride")
     if params.is_cuda and nat.native_enabled():
         lib = nat.require(params.device)
         a = nat.OptArgs(nat.ptr(params), nat.ptr(m), nat.ptr(v), nat.ptr(step), nat.ptr(grad),
                         nat.ptr(loss_log), 0 if loss_log is None else loss_log.shape[0], n_models, P, cfg.kind,
-                        loss_scale, 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow))
+                        loss_scale, 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow),
+                        0 if shadow is None else shadow.stride(0))
         nat.check(lib.dtp_flat_optimizer(ctypes.byref(a), nat.stream_ptr()), "dtp_flat_optimizer")
         return
     g = grad[: n_models * P].view(n_models, P) * grad_scale
@@ -99,7 +101,7 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
             loss_log[t % loss_log.shape[0], i] = grad[n_models * P + i] * loss_scale
         step[i] = t + 1
     if shadow is not None:
-        shadow.copy_(params)
+        shadow[:, :P].copy_(params)
 
 
 class FlatOptimizer:
@@ -137,7 +139,7 @@ class FlatOptimizer:
         sh = self.shadow
         fresh = sh is not None and sh._token == sh._current()  # else the next forward re-casts anyway
         flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.cfg, slope=self.slope,
-                            shadow=sh.buf.view(self.params.shape) if fresh else None)
+                            shadow=sh.buf if fresh else None)
         if fresh:
             sh.mark_fresh()
 

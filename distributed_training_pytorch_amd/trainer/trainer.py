@@ -469,13 +469,13 @@ class Trainer:
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
         last = None
-        # steady-state clock: from the end of the first launch on (engine set-up, first
-        # kernel loads and the prologue of a fresh launch excluded); every launch ends in
-        # a loss readback, so the clock starts and stops on a synchronised device
+        # steady-state clock: the first launch runs _STEADY_AFTER steps (engine set-up and
+        # first kernel loads), the clock runs from its end; every launch ends in a loss
+        # readback, so the clock starts and stops on a synchronised device
         steady_t0, steady_from = None, None
         try:
             while self.global_step < total:
-                n = min(tr.cfg.steps_per_launch, total - self.global_step)
+                n = min(tr.cfg.steps_per_launch if steady_t0 is not None else _STEADY_AFTER, total - self.global_step)
                 if self.every_n_train_steps:
                     n = min(n, self.every_n_train_steps - self.global_step % self.every_n_train_steps)
                 s0 = self.global_step
