@@ -6,8 +6,8 @@ Linears are real GEMMs.
   ours  : ModelBank(2, hidden=W) -- every Linear on csrc/gemm.hip (bias/LeakyReLU
           epilogues, activation gradient fused into the dx GEMM), bf16 compute with
           fp32 master weights; FlatDDP (bucketed RCCL / xGMI all-reduce from the
-          backward hooks); FlatOptimizer (one Adam launch for both models, which also
-          writes the bf16 weight operands: ops/gemm.py ComputeShadow)
+          backward hooks); FlatOptimizer (one Adam launch for both models; with
+          --shadow it also writes the bf16 weight operands, ops/gemm.py ComputeShadow)
   stock : nn.Sequential + torch.autocast(bf16) + torch DDP + torch.optim.Adam
           (hipBLASLt GEMMs, ATen elementwise) -- the same math on stock PyTorch-ROCm
 
@@ -39,9 +39,11 @@ def run_ours(a, X, Y, dev, world):
     torch.manual_seed(0)
     bank = ModelBank(2, hidden=a.width, depth=a.depth, compute_dtype=torch.bfloat16).to(dev)
     ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad, comm="rccl") if world > 1 else None
-    # Adam also writes the bf16 weight operands (no per-forward casts); --no-shadow: cast each forward
+    # --shadow: Adam also writes the bf16 weight operands (no per-forward casts). Measured
+    # at W = 4096 / 2048 / 1024: 4.52 / 1.78 / 1.28 ms vs 4.56 / 1.75 / 1.28 casting each
+    # forward (profiles/r3_shadow/), so the cast stays the default
     opt = FlatOptimizer(bank.flat, bank.flat_grad, OptimConfig(lr=1e-3),
-                        shadow=None if a.no_shadow else bank.compute_shadow())
+                        shadow=bank.compute_shadow() if a.shadow else None)
     mse = torch.nn.MSELoss()
     fwd = ddp if ddp is not None else bank
 
@@ -97,7 +99,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--impl", choices=["ours", "stock", "both"], default="both")
-    ap.add_argument("--no-shadow", action="store_true", help="ours: cast the fp32 masters to bf16 every forward")
+    ap.add_argument("--shadow", action="store_true",
+                    help="ours: the Adam kernel writes the bf16 weight operands (ops/gemm.py ComputeShadow) "
+                         "instead of a cast before every forward")
     ap.add_argument("--gemm-backend", choices=["auto", "mfma", "blaslt"], default=None,
                     help="ops/gemm.py backend for our implementation (default: DTP_GEMM_BACKEND or auto)")
     a = ap.parse_args()
@@ -131,7 +135,7 @@ def main():
                               "samples_per_s": a.batch * world * a.steps / dt, "model_tflops": flops / dt / 1e12,
                               "dtype": "bf16 compute, fp32 master weights",
                               "gemm_backend": gemm_mod.get_backend() if impl == "ours" else "torch",
-                              "weight_shadow": (not a.no_shadow) if impl == "ours" else None,
+                              "weight_shadow": a.shadow if impl == "ours" else None,
                               "tuned": {"x".join(map(str, k[:3])) + ("T" if k[3] else "N") + ("T" if k[4] else "N")
                                         + ("+acc" if k[9] else "") + ("+aux" if k[7] else "") + ("+act" if k[8] else ""):
                                         v for k, v in gemm_mod.tuned_choices().items()} if impl == "ours" else {}}),
