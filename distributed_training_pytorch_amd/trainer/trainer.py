@@ -470,9 +470,22 @@ class Trainer:
         t0 = time.perf_counter()
         last = None
         # steady-state clock: the first launch runs _STEADY_AFTER steps (engine set-up and
-        # first kernel loads), the clock runs from its end; every launch ends in a loss
-        # readback, so the clock starts and stops on a synchronised device
+        # first kernel loads), the clock runs from its end (synchronised by its loss readback)
         steady_t0, steady_from = None, None
+        # launch k+1 is queued before launch k's loss rows are waited for and written
+        # (losses_async: a pinned copy + event behind launch k), so the CSV writing
+        # overlaps the next launch instead of idling the GPU
+        pending = None
+
+        def drain(p):
+            nonlocal last
+            s0_, s1_, handle = p
+            rows = handle.wait()
+            every = self.log_every_n_steps
+            first = -(s0_ + 1) % every  # index of the first logged step of the launch
+            logger.log_rows(list(range(s0_ + first + 1, s1_ + 1, every)), names, rows[first::every])
+            last = rows[-1]
+
         try:
             while self.global_step < total:
                 n = min(tr.cfg.steps_per_launch if steady_t0 is not None else _STEADY_AFTER, total - self.global_step)
@@ -481,20 +494,27 @@ class Trainer:
                 s0 = self.global_step
                 tr.train(n)
                 self.global_step += n
-                rows = tr.losses(s0, self.global_step).tolist()  # one readback per launch
-                every = self.log_every_n_steps
-                first = -(s0 + 1) % every  # index of the first logged step of this launch
-                logger.log_rows(list(range(s0 + first + 1, self.global_step + 1, every)), names, rows[first::every])
-                last = rows[-1]
+                handle = tr.losses_async(s0, self.global_step)
+                if pending is not None:
+                    drain(pending)
+                pending = (s0, self.global_step, handle)
                 if steady_t0 is None:
+                    drain(pending)
+                    pending = None
                     steady_t0, steady_from = time.perf_counter(), self.global_step
                 # PL's bookkeeping: the batch that reaches max_steps ends the fit inside its
                 # epoch (epoch e, batch_in_epoch = its index + 1), it does not open the next
                 e, b = divmod(self.global_step - 1, spe)
                 self.current_epoch, self._batch_in_epoch = e, b + 1
                 if self.every_n_train_steps and self.global_step % self.every_n_train_steps == 0:
+                    if pending is not None:
+                        drain(pending)
+                        pending = None
                     self._export_fused_state(tr, models, opts)
                     self._save(model, opts, "last.ckpt")
+            if pending is not None:
+                drain(pending)
+                pending = None
             torch.cuda.synchronize(self.device)
             t1 = time.perf_counter()
             self.fit_time = t1 - t0
