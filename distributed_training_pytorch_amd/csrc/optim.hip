@@ -24,25 +24,45 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
   float* v = a.opt_v ? a.opt_v + (size_t)model * a.P : nullptr;
   const float* g = a.grad + (size_t)model * a.P;
   __bf16* sh = a.shadow ? reinterpret_cast<__bf16*>(a.shadow) + (size_t)model * a.shadow_ld : nullptr;
-  // rows of 16-byte aligned float4s when every model row is (P % 4 == 0): 4 elements
-  // per thread and load (the update is HBM-bound: 28 B per parameter)
-  const bool vec = (a.P & 3) == 0 && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)g | (uintptr_t)(v ? v : p)) & 15) == 0 &&
-                   ((uintptr_t)sh & 7) == 0;
+  // float4 body: the four rows share their offset within 16 bytes (same [n][P] layout
+  // on 16-byte aligned bases), so `head` scalar elements (0-3) bring every row to a
+  // 16-byte boundary, the body runs 4 elements per thread and load, and at most 3
+  // elements remain (the update is HBM-bound: 28 B per parameter). With an odd P the
+  // second model's row starts off a 16-byte boundary: before the head peel it ran
+  // the element-wise loop.
+  const uintptr_t ph = (uintptr_t)p & 15;
+  const bool vec = v && (((uintptr_t)m & 15) == ph) && (((uintptr_t)v & 15) == ph) && (((uintptr_t)g & 15) == ph) &&
+                   (ph & 3) == 0 && (!sh || (ph == 0 && (a.P & 3) == 0 && ((uintptr_t)sh & 7) == 0));
   if (a.kind == DTP_MODE_ADAM && vec) {
     const AdamScalars s = adam_scalars(a.hp, t + 1);
-    const int P4 = a.P >> 2;
+    const int head = min((int)((16 - ph) & 15) >> 2, a.P);
+    const int P4 = (a.P - head) >> 2, tail0 = head + 4 * P4;
+    float4* p4 = reinterpret_cast<float4*>(p + head);
+    float4* m4 = reinterpret_cast<float4*>(m + head);
+    float4* v4 = reinterpret_cast<float4*>(v + head);
+    const float4* g4 = reinterpret_cast<const float4*>(g + head);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < P4; i += gridDim.x * kBlock) {
-      float4 w = reinterpret_cast<float4*>(p)[i], mi = reinterpret_cast<float4*>(m)[i];
-      float4 vi = reinterpret_cast<float4*>(v)[i];
-      const float4 gi = reinterpret_cast<const float4*>(g)[i];
+      float4 w = p4[i], mi = m4[i], vi = v4[i];
+      const float4 gi = g4[i];
       adam_update(w.x, mi.x, vi.x, gi.x * a.hp.grad_scale, s);
       adam_update(w.y, mi.y, vi.y, gi.y * a.hp.grad_scale, s);
       adam_update(w.z, mi.z, vi.z, gi.z * a.hp.grad_scale, s);
       adam_update(w.w, mi.w, vi.w, gi.w * a.hp.grad_scale, s);
-      reinterpret_cast<float4*>(p)[i] = w;
-      reinterpret_cast<float4*>(m)[i] = mi;
-      reinterpret_cast<float4*>(v)[i] = vi;
+      p4[i] = w;
+      m4[i] = mi;
+      v4[i] = vi;
       if (sh) reinterpret_cast<bf16x4*>(sh)[i] = bf16x4{(__bf16)w.x, (__bf16)w.y, (__bf16)w.z, (__bf16)w.w};
+    }
+    // the head and tail elements (at most 6), one per thread of the first block
+    const int e = blockIdx.x == 0 ? (int)threadIdx.x : 1 << 30;
+    const int idx = e < head ? e : (e - head < a.P - tail0 ? tail0 + e - head : -1);
+    if (idx >= 0) {
+      float w = p[idx], mi = m[idx], vi = v[idx];
+      adam_update(w, mi, vi, g[idx] * a.hp.grad_scale, s);
+      p[idx] = w;
+      m[idx] = mi;
+      v[idx] = vi;
+      if (sh) sh[idx] = (__bf16)w;
     }
   } else if (a.kind == DTP_MODE_ADAM && sh) {
     // unaligned rows (odd P: every bias-terminated MLP) with a shadow: two elements per
