@@ -235,24 +235,33 @@ def test_fused_trainer_torch_sampler_order():
     torch.testing.assert_close(tr.params, ref_p, rtol=1e-3, atol=2e-5)
 
 
-def test_flat_optimizer_matches_torch_adam():
-    P = 371
-    p0 = torch.randn(2, P, device=DEV)
-    ps = [torch.nn.Parameter(p0[i].clone()) for i in range(2)]
+@pytest.mark.parametrize("n,P,shadow", [(2, 371, False), (4, 371, False), (4, 370, False), (3, 3, False),
+                                         (4, 20001, False), (3, 20002, False), (2, 20000, True), (2, 371, True),
+                                         (3, 20001, True)])
+def test_flat_optimizer_matches_torch_adam(n, P, shadow):
+    """Every row phase of the float4 body (P % 4 = 0..3 over n rows: head peels of 0-3
+    elements), rows shorter than a head (P = 3), the multi-block launch (P > 4096), and
+    the bf16 shadow write (float4 path when P % 4 == 0, bf16-pair path otherwise)."""
+    p0 = torch.randn(n, P, device=DEV)
+    ps = [torch.nn.Parameter(p0[i].clone()) for i in range(n)]
     opt = torch.optim.Adam(ps, lr=1e-3)
     params = p0.clone()
     m = torch.zeros_like(params)
     v = torch.zeros_like(params)
-    step = torch.zeros(2, dtype=torch.int32, device=DEV)
+    step = torch.zeros(n, dtype=torch.int32, device=DEV)
+    sh = torch.full((n, -(-P // 256) * 256), float("nan"), dtype=torch.bfloat16, device=DEV) if shadow else None
     for t in range(5):
-        g = torch.randn(2, P, device=DEV)
-        for i in range(2):
+        g = torch.randn(n, P, device=DEV)
+        for i in range(n):
             ps[i].grad = g[i].clone()
         opt.step()
-        buf = torch.cat([g.reshape(-1), torch.zeros(2, device=DEV)])
-        flat_optimizer_step(params, m, v, step, buf, OptimConfig())
+        buf = torch.cat([g.reshape(-1), torch.zeros(n, device=DEV)])
+        flat_optimizer_step(params, m, v, step, buf, OptimConfig(), shadow=sh)
+        if shadow:
+            assert torch.equal(sh[:, :P], params.to(torch.bfloat16))
+            assert torch.isnan(sh[:, P:].float()).all()  # the row padding is never written
     torch.testing.assert_close(params, torch.stack([p.detach() for p in ps]), rtol=1e-5, atol=1e-6)
-    assert step.tolist() == [5, 5]
+    assert step.tolist() == [5] * n
 
 
 def test_toy_model_autograd_path_matches_cpu():
