@@ -130,7 +130,9 @@ def main():
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm,
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
-                    else "Feistel shuffle", "cu_mask": a.cu_mask}
+                    else "Feistel shuffle", "cu_mask": a.cu_mask,
+                    # lanes per sample of the fused step (1, or 2 / 4: csrc/mlp_lanes.h for batches <= 128 / 64)
+                    "lanes_per_sample": runner.lanes}
 
     # the timed region is bracketed by an all-rank barrier + synchronize on both sides;
     # ranks of the in-kernel xGMI engine use the framework's device barrier (one xGMI

@@ -228,6 +228,9 @@ def _declare(lib):
         "dtp_train_engine_create": (c_void_p, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
         "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_int, c_void_p]),
         "dtp_train_engine_destroy": (None, [c_void_p]),
+        "dtp_train_engine_lanes": (c_int, [c_void_p]),
+        "dtp_mlp_train_lanes": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
+        "dtp_mlp_train_profile_lanes": (c_int, [P(TrainArgs), c_int, c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),

@@ -58,6 +58,9 @@ int dtp_mlp_workspace_floats(int in, int h, int nl, int out);
 int dtp_mlp_train_bf16_supported(int in, int h, int nl, int out);
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream);
 int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream);
+int dtp_mlp_train_profile_lanes(const DtpTrainArgs* a, int lanes, void* stream);
+// lanes per sample of the step instance these arguments select (mlp_lanes.h), 0: none
+int dtp_mlp_train_lanes(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode);
 long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world);
 
 // ---- stage forward / backward (autograd path, layer-split pipeline) ----

@@ -15,6 +15,7 @@
 
 #include "dtp_api.h"
 #include "mlp_core.h"
+#include "mlp_lanes.h"
 #include "mlp_pipe.h"
 #include "mlp_scalar.h"
 #include "optim_core.h"
@@ -500,6 +501,361 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
 }
 
 // ------------------------------------------------------------------------------
+// Several lanes per sample (mlp_lanes.h): the step for per-rank batches <= 256 / L.
+// floats of dataset staged in LDS by the lanes kernel (strong scaling: n = 512 x 3)
+constexpr int kLaneData = 4096;
+
+template <class S, int L>
+struct LaneSmem {
+  using C = LaneCfg<S, L>;
+  alignas(16) float wb[C::pad4(C::LW)];
+  alignas(16) float stg[kWaves][Scal<S>::NT][2 * C::AREA];  // per wave, per tile: dz area, h area
+  alignas(16) float red[kWaves][Scal<S>::NT * 256];         // per-wave partial dW tiles
+  alignas(16) float2 adam_tab[kAdamTab];
+  alignas(16) float data[kLaneData];
+  float sink[4];
+};
+
+template <class S, int L, int MODE, bool PROF = false>
+__global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(DtpTrainArgs a) {
+  using SC = Scal<S>;
+  using C = LaneCfg<S, L>;
+  constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT, NO = C::NO, TS = C::TS, H = S::H;
+  constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM;
+  static_assert(MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM, "the lanes step serves the Adam modes");
+  __shared__ __align__(16) LaneSmem<S, L> sm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int model = blockIdx.x;
+  const int part = lane & (L - 1);          // this lane's slice of every hidden layer
+  const int ws = lane / L;                  // sample slot inside the wave
+  const int bk = wave * C::G + ws;          // batch position of this lane's sample
+  unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
+  const float slope = a.hp.slope;
+
+  // ---- prologue (all global reads issued before the first wait, as in mlp_train_kernel)
+  float* __restrict__ gp = a.params + (size_t)model * P;
+  const SamplerCfg smp = a.smp;
+  int pf[NPT], pb[NPT], tp[NPT];
+  float pw[NPT], mr[NPT], vr[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = NPT * tid + k;
+    lane_pos<C, S>(p < P ? p : 0, pf[k], pb[k], tp[k]);
+    const bool own = p < P;
+    pw[k] = own ? gp[p] : 0.f;
+    mr[k] = own ? a.opt_m[(size_t)model * P + p] : 0.f;
+    vr[k] = own ? a.opt_v[(size_t)model * P + p] : 0.f;
+  }
+  const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
+  int epoch = t0 / smp.steps_per_epoch;
+  int bi = t0 - epoch * smp.steps_per_epoch;
+  auto fast_index = [&](int ep_, int b_) -> int {
+    const int start = b_ * smp.batch;
+    const int size = min(smp.batch, smp.num_samples - start);
+    int q = smp.rank + (start + bk) * smp.world;
+    q = q >= smp.n ? q - smp.n : q;
+    q = q < smp.n ? q : smp.n - 1;
+    const int di = table_epoch(smp, ep_)[q];
+    return bk < size ? di : -1;
+  };
+  auto roll = [&](int& ep_, int& b_) {
+    const bool r_ = ++b_ == smp.steps_per_epoch;
+    b_ = r_ ? 0 : b_;
+    ep_ += r_ ? 1 : 0;
+  };
+  int e2 = epoch, b2 = bi;
+  const int fidx0 = fast_index(epoch, bi);
+  roll(e2, b2);
+  int fidx = fast_index(e2, b2);
+  unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
+  for (int e = tid; e < C::pad4(C::LW); e += kBlock) sm.wb[e] = 0.f;
+  for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
+  for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * S::IN + e] = a.Y[e];
+  const int yoff = smp.n * S::IN;
+  // this wave's staging areas: zero (unwritten rows / columns stay finite), then the
+  // constant-1 bias columns of every tile, written once per launch
+  {
+    float* s0 = &sm.stg[wave][0][0];
+    for (int e = lane; e < NT * 2 * C::AREA; e += kWave) s0[e] = 0.f;
+    static_for<0, NL>([&](auto LC) {
+      constexpr int l = decltype(LC)::value;
+      constexpr int col = SC::coloff(l) + S::din(l);
+      float* hb = &sm.stg[wave][SC::tile(l)][C::AREA];
+      for (int e = lane; e < 4 * TS; e += kWave) hb[(e / TS) * C::QS + col * TS + e % TS] = 1.f;
+    });
+  }
+  __syncthreads();  // weight blocks zeroed (pads stay 0) before the owners scatter into them
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    if (NPT * tid + k < P) {
+      sm.wb[pf[k]] = pw[k];
+      if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
+    }
+  }
+  int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
+  auto fast_gather = [&](int di, float (&x)[S::IN], float (&y)[S::OUT]) {
+    const bool v = di >= 0;
+    di = (unsigned)di < (unsigned)smp.n ? di : 0;
+    static_for<0, S::IN>([&](auto IC) {
+      constexpr int i = decltype(IC)::value;
+      const float t_ = sm.data[di * S::IN + i];
+      x[i] = v ? t_ : 0.f;
+    });
+    static_for<0, S::OUT>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      const float t_ = sm.data[yoff + di * S::OUT + j];
+      y[j] = v ? t_ : 0.f;
+    });
+    return v;
+  };
+  float nx[S::IN], ny[S::OUT];
+  bool nvalid = fast_gather(fidx0, nx, ny);
+  auto fill_adam = [&](int base) {
+    const int n = min(kAdamTab, a.n_steps - base);
+    for (int e = tid; e < n; e += kBlock) {
+      const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
+      const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
+      sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
+    }
+  };
+  fill_adam(0);
+  // per-lane LDS bases: the part's slice of the partitioned blocks, the sample's slot in a
+  // staged operand (+ the part's first column), the MFMA reader's operands
+  const float* const wlp = sm.wb + part * C::NOP;
+  const int wslot = (ws & 3) * C::QS + (ws >> 2);
+  const int wpart = wslot + part * NO * TS;
+  const int rdoff = (lane >> 4) * C::QS + (lane & 15) * TS;
+  // is slot k of this lane's slice a real unit (k*L + part < H)?
+  auto slot_ok = [&](int k) { return C::EXACT || part * NO + k < H; };
+  __syncthreads();
+
+  for (int it = 0; it < a.n_steps; ++it) {
+    DTP_STAMP(0);
+    const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
+    const float inv = 1.f / (float)(bsz * S::OUT);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool valid = nvalid;
+    LaneAct<C> st;
+    static_for<0, S::IN>([&](auto IC) { st.hin[decltype(IC)::value] = nx[decltype(IC)::value]; });
+    float x0[S::IN];
+    static_for<0, S::IN>([&](auto IC) { x0[decltype(IC)::value] = nx[decltype(IC)::value]; });
+
+    // ---------------- forward
+    LLast<C> last;
+    LBBlk<C, NL - 1> bt;
+    LBBlk<C, NL - 2> bt2;
+    float out[16];
+    {
+      LFBlk<C, 0> b0;
+      b0.template load<0, LFBlk<C, 0>::NR>(sm.wb, wlp);
+      DTP_STAMP(1);
+      lane_forward<C, 0>(sm.wb, wlp, b0, st, slope, last, bt, bt2, out);
+    }
+    // ---------------- loss (MSE) -> output gradient (every lane of the sample)
+    float dzl[S::OUT];
+    float lpart = 0.f;
+    static_for<0, S::OUT>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      const float d = out[j] - ny[j];
+      lpart = valid ? fmaf(d, d, lpart) : lpart;
+      dzl[j] = valid ? 2.f * d * inv : 0.f;
+    });
+    DTP_STAMP(2);
+
+    // ---------------- backward
+    float dzp[C::NOP];  // this lane's slice of the current layer's output gradient
+    {  // last layer: stage (dz, loss, own slice of its input), input-gradient slice
+      constexpr int l = NL - 1;
+      float* tl = &sm.stg[wave][SC::tile(l)][0];
+      if (part == 0) {
+        static_for<0, S::OUT>([&](auto JC) {
+          tl[wslot + (SC::rowoff(l) + decltype(JC)::value) * TS] = dzl[decltype(JC)::value];
+        });
+        tl[wslot + SC::lossrow() * TS] = lpart;
+      }
+      static_for<0, NO>([&](auto KC) {
+        constexpr int k = decltype(KC)::value;
+        if (slot_ok(k)) tl[C::AREA + wpart + (SC::coloff(l) + k) * TS] = st.own[l - 1][k];
+      });
+      f32x2 g[C::NPR];
+      static_for<0, C::NPR>([&](auto RC) { g[decltype(RC)::value] = f32x2{0.f, 0.f}; });
+      static_for<0, S::OUT>([&](auto OC) {
+        constexpr int o = decltype(OC)::value;
+        const f32x2 d = f32x2{dzl[o], dzl[o]};
+        static_for<0, C::NPR>([&](auto RC) {
+          constexpr int r = decltype(RC)::value;
+          g[r] = __builtin_elementwise_fma(quad_pair<r % 2>(bt.w[o][r / 2]), d, g[r]);
+        });
+      });
+      static_for<0, NO>([&](auto KC) {
+        constexpr int k = decltype(KC)::value;
+        const float v = (k & 1) ? g[k / 2].y : g[k / 2].x;
+        dzp[k] = v * leaky_grad_from_out(st.own[l - 1][k], slope);
+      });
+      if constexpr (!SC::PACK) {
+        __builtin_amdgcn_wave_barrier();
+        const auto to = lane_tile_ops<C>(tl, rdoff);
+        f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+        static_for<0, TS>([&](auto KC) { lane_kstep<decltype(KC)::value>(to, acc[SC::tile(l)], a1); });
+        acc[SC::tile(l)] += a1;
+      }
+    }
+    // hidden layers NL-2 .. 1: block B of layer l in registers, block l-1 prefetched
+    auto hidden = [&](auto LC, const auto& B, auto& nb) {
+      constexpr int l = decltype(LC)::value;
+      float* tl = &sm.stg[wave][SC::tile(l)][0];
+      static_for<0, NO>([&](auto KC) {
+        constexpr int k = decltype(KC)::value;
+        if (slot_ok(k)) {
+          tl[wpart + (SC::rowoff(l) + k) * TS] = dzp[k];
+          tl[C::AREA + wpart + (SC::coloff(l) + k) * TS] = st.own[l - 1][k];
+        }
+      });
+      __builtin_amdgcn_wave_barrier();
+      const auto to = lane_tile_ops<C>(tl, rdoff);
+      float dzf[16];
+      static_for<0, C::L>([&](auto PC) {
+        constexpr int pp = decltype(PC)::value;
+        static_for<0, NO>([&](auto KC) {
+          constexpr int k = decltype(KC)::value;
+          if constexpr (pp * NO + k < H) dzf[pp * NO + k] = part_bcast<C::L, pp>(dzp[k]);
+        });
+      });
+      f32x2 g[C::NPR];
+      static_for<0, C::NPR>([&](auto RC) { g[decltype(RC)::value] = f32x2{0.f, 0.f}; });
+      f32x4 a0 = acc[SC::tile(l)], a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      constexpr int J0 = 2;
+      LNone none;
+      static_for<0, H>([&](auto OC) {
+        constexpr int o = decltype(OC)::value;
+        if constexpr (o >= J0) {
+          constexpr int k0 = TS * (o - J0) / (H - J0), k1 = TS * (o - J0 + 1) / (H - J0);
+          static_for<k0, k1>([&](auto KC) { lane_kstep<decltype(KC)::value>(to, a0, a1); });
+        }
+        const f32x2 d = f32x2{dzf[o], dzf[o]};
+        static_for<0, C::NPR>([&](auto RC) {
+          constexpr int r = decltype(RC)::value;
+          g[r] = __builtin_elementwise_fma(quad_pair<r % 2>(B.w[o][r / 2]), d, g[r]);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        lchunk<o, H>(sm.wb, wlp, nb, none);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      acc[SC::tile(l)] = a0 + a1;
+      static_for<0, NO>([&](auto KC) {
+        constexpr int k = decltype(KC)::value;
+        const float v = (k & 1) ? g[k / 2].y : g[k / 2].x;
+        dzp[k] = v * leaky_grad_from_out(st.own[l - 1][k], slope);
+      });
+    };
+    auto hidden_rest = [&](auto self, auto LC, const auto& B) -> void {
+      constexpr int l = decltype(LC)::value;
+      if constexpr (l > 1) {
+        LBBlk<C, l - 1> nb;
+        hidden(LC, B, nb);
+        self(self, std::integral_constant<int, l - 1>{}, nb);
+      } else {
+        LNone none;
+        hidden(LC, B, none);
+      }
+    };
+    hidden_rest(hidden_rest, std::integral_constant<int, NL - 2>{}, bt2);
+    {  // layer 0: its dW tile only (packed with the last layer's when they fit)
+      float* tl = &sm.stg[wave][SC::tile(0)][0];
+      static_for<0, NO>([&](auto KC) {
+        constexpr int k = decltype(KC)::value;
+        if (slot_ok(k)) tl[wpart + (SC::rowoff(0) + k) * TS] = dzp[k];
+      });
+      if (part == 0) {
+        static_for<0, S::IN>([&](auto IC) {
+          tl[C::AREA + wslot + (SC::coloff(0) + decltype(IC)::value) * TS] = x0[decltype(IC)::value];
+        });
+      }
+      __builtin_amdgcn_wave_barrier();
+      const auto to = lane_tile_ops<C>(tl, rdoff);
+      f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      static_for<0, TS>([&](auto KC) { lane_kstep<decltype(KC)::value>(to, acc[SC::tile(0)], a1); });
+      acc[SC::tile(0)] += a1;
+    }
+    DTP_STAMP(8 + wave);
+    DTP_STAMP(3);
+    {
+      const int q = lane >> 4, col = lane & 15;
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.red[wave][tt * 256 + (4 * q + r) * 16 + col] = acc[tt][r];
+      }
+    }
+    __syncthreads();
+    const float2 adam_sc = sm.adam_tab[it % kAdamTab];
+    DTP_STAMP(4);
+    float g[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) s += sm.red[ww][tp[k]];
+      g[k] = s;
+    }
+    float lsum = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) lsum += sm.red[ww][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+    const float mean_loss = lsum * inv;
+    DTP_STAMP(5);
+    float gloss = mean_loss;
+    if constexpr (kXgmi) {
+      xepoch += 1u;
+      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid);
+    }
+    const int lslot_now = lslot;
+    roll(epoch, bi);
+    if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
+    nvalid = fast_gather(fidx, nx, ny);
+    roll(e2, b2);
+    fidx = fast_index(e2, b2);
+    {
+      AdamScalars as = adam_consts(a.hp);
+      as.step_size = adam_sc.x;
+      as.bc2_sqrt = adam_sc.y;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const bool own = NPT * tid + k < P;
+        *(own ? &sm.wb[pf[k]] : &sm.sink[0]) = pw[k];
+        *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
+      }
+    }
+    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, kBlock) : 0) && a.loss_log) {
+      const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
+      a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
+    }
+    DTP_STAMP(6);
+    __syncthreads();
+    if ((it + 1) % kAdamTab == 0 && it + 1 < a.n_steps) {
+      fill_adam(it + 1);
+      __syncthreads();
+    }
+    DTP_STAMP(7);
+  }
+
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = NPT * tid + k;
+    if (p < P) {
+      gp[p] = pw[k];
+      a.opt_m[(size_t)model * P + p] = mr[k];
+      a.opt_v[(size_t)model * P + p] = vr[k];
+    }
+  }
+  if (tid == 0) a.step[model] = t0 + a.n_steps;
+  if (kXgmi && tid == 0) a.epoch[model] = xepoch;
+}
+
+// ------------------------------------------------------------------------------
 __global__ void sampler_probe_kernel(SamplerCfg s, long long t0, int n_steps, int* out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   const int st = blockIdx.y;
@@ -570,8 +926,44 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   X(2, 10, 5, 1)                 \
   X(2, 10, 5, 4)
 
-TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode) {
+template <class S, int L, int MODE>
+void launch_lanes(const DtpTrainArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, MODE>), dim3(a.n_models), dim3(dtp::kBlock), 0, st, a);
+}
+
+template <class S, int L>
+TrainLaunchFn lanes_fn(int mode) {
+  if (mode == DTP_MODE_ADAM) return &launch_lanes<S, L, DTP_MODE_ADAM>;
+  if (mode == DTP_MODE_XGMI_ADAM) return &launch_lanes<S, L, DTP_MODE_XGMI_ADAM>;
+  return nullptr;
+}
+
+// lanes per sample of the step instance for this launch: 4 for per-rank batches <= 64,
+// 2 for <= 128, else 1 (the one-lane kernel).  DTP_LANES=1|2|4 forces a choice (A/B
+// runs; a forced L whose batch bound does not hold falls back to 1).
+int pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
+  static const int forced = [] {
+    const char* e = getenv("DTP_LANES");
+    return e ? atoi(e) : 0;
+  }();
+  if (!fast || a.bf16 || a.smp.n * (in + out) > dtp::kLaneData) return 1;
+  int want = a.smp.batch <= dtp::kBlock / 4 ? 4 : (a.smp.batch <= dtp::kBlock / 2 ? 2 : 1);
+  if (forced == 1 || forced == 2 || forced == 4) want = forced;
+  return a.smp.batch <= dtp::kBlock / want ? want : 1;
+}
+
+TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode, int* lanes = nullptr) {
   const bool fast = fast_path_ok(a, in, out, mode);
+  const int L = pick_lanes(a, in, out, fast);
+  if (lanes) *lanes = L;
+  if (L > 1) {
+#define X(I, H, N, O)                                                                                   \
+  if (in == I && h == H && nl == N && out == O)                                                         \
+    return L == 4 ? lanes_fn<dtp::Stage<I, H, N, O, false>, 4>(mode) : lanes_fn<dtp::Stage<I, H, N, O, false>, 2>(mode);
+    DTP_TRAIN_SHAPES(X)
+#undef X
+    if (lanes) *lanes = 1;
+  }
   if (a.bf16) {
 #define X(I, H, N, O) \
   if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false, true>>(mode, fast);
@@ -616,6 +1008,7 @@ struct TrainEngine {
   DtpTrainArgs a;
   TrainLaunchFn fn;
   int mode;
+  int lanes;  // lanes per sample of the chosen instance (1: mlp_train_kernel)
 };
 
 template <class S>
@@ -625,6 +1018,16 @@ int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
   hipLaunchKernelGGL((dtp::mlp_train_kernel<S, DTP_MODE_ADAM, true, true>), dim3(a->n_models), dim3(dtp::kBlock), 0,
                      st, *a);
   return check_launch("mlp_train_kernel<prof>");
+}
+
+template <class S, int L>
+int launch_lanes_profile(const DtpTrainArgs* a, hipStream_t st) {
+  if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM) || a->smp.batch > dtp::kBlock / L ||
+      a->smp.n * (S::IN + S::OUT) > dtp::kLaneData)
+    return set_err(-2, "the lanes profile instance needs the FAST configuration and batch <= 256 / L");
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, true>), dim3(a->n_models), dim3(dtp::kBlock),
+                     0, st, *a);
+  return check_launch("mlp_train_lanes_kernel<prof>");
 }
 
 }  // namespace
@@ -675,7 +1078,8 @@ int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mod
 
 void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
   if (validate_train(a, mode)) return nullptr;
-  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode);
+  int lanes = 1;
+  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode, &lanes);
   if (!fn) {
     set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
     return nullptr;
@@ -684,7 +1088,21 @@ void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int 
   e->a = *a;
   e->fn = fn;
   e->mode = mode;
+  e->lanes = lanes;
   return e;
+}
+
+// lanes per sample of the engine's kernel instance (1 = one lane per sample)
+int dtp_train_engine_lanes(void* h) {
+  auto* e = static_cast<TrainEngine*>(h);
+  return e ? e->lanes : set_err(-1, "null engine");
+}
+
+// lanes per sample the step would use for these arguments (0: no fused instance)
+int dtp_mlp_train_lanes(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
+  if (validate_train(a, mode)) return 0;
+  int lanes = 1;
+  return resolve_train(*a, in, h, nl, out, mode, &lanes) ? lanes : 0;
 }
 
 // n_steps iterations in ONE persistent launch on `stream`, starting at step t0 (the
@@ -705,6 +1123,13 @@ void dtp_train_engine_destroy(void* h) { delete static_cast<TrainEngine*>(h); }
 // diagnostic: toy shape, Adam, phase stamps into a->status (as u64[n_models][8][16])
 int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream) {
   return launch_train_profile<dtp::Stage<2, 10, 5, 1, false>>(a, (hipStream_t)stream);
+}
+
+// same for the lanes step (toy shape), L = 2 or 4
+int dtp_mlp_train_profile_lanes(const DtpTrainArgs* a, int lanes, void* stream) {
+  if (lanes == 2) return launch_lanes_profile<dtp::Stage<2, 10, 5, 1, false>, 2>(a, (hipStream_t)stream);
+  if (lanes == 4) return launch_lanes_profile<dtp::Stage<2, 10, 5, 1, false>, 4>(a, (hipStream_t)stream);
+  return set_err(-1, "lanes must be 2 or 4");
 }
 
 int dtp_sampler_indices(const dtp::SamplerCfg* s, long long t0, int n_steps, int* out, void* stream) {

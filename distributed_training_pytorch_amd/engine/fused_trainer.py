@@ -118,6 +118,17 @@ class FusedTrainer:
         if self.comm == "xgmi":
             self._setup_xgmi()
 
+    @property
+    def lanes(self) -> int:
+        """Lanes per sample of the fused step instance this engine launches: 1 = the
+        one-lane kernel, 2 / 4 = the several-lanes step (``csrc/mlp_lanes.h``) that the
+        native dispatch picks for per-rank batches <= 128 / <= 64 (0: no fused kernel,
+        e.g. a CPU engine or the RCCL path's grad kernel)."""
+        if not self.native or self.comm in ("rccl", "host"):
+            return 0
+        a = self._train_args(1, self._update_mode(), None)
+        return int(nat.load().dtp_mlp_train_lanes(ctypes.byref(a), *self.spec.key[:4], self._update_mode()))
+
     # ------------------------------------------------------------------ setup
     def _resolve_comm(self) -> str:
         c = self.cfg.comm

@@ -213,6 +213,7 @@ class LayerSplitDDP:
         self._pending: list = []
         self._queued = False
         self._done: set = set()
+        self._fired = False  # a grad-ready hook fired since the last join
 
     def _setup_xgmi(self, strict: bool):
         from .xgmi import XgmiAllReduce
@@ -237,6 +238,7 @@ class LayerSplitDDP:
             raise RuntimeError(f"LayerSplitDDP comm='xgmi' unavailable: {why or 'a peer failed'}")
 
     def _hook(self, p):
+        self._fired = True
         if not self._queued:
             torch.autograd.Variable._execution_engine.queue_callback(self.finish)
             self._queued = True
@@ -267,11 +269,16 @@ class LayerSplitDDP:
             self._pending.append((None, i))
 
     def finish(self):
-        """Join every bucket's reduction (idempotent; also the end-of-backward callback)."""
-        for i in range(len(self.params)):  # stages that produced no gradient this backward
-            if i not in self._done:
-                self._done.add(i)
-                self._reduce(i)
+        """Join every bucket's reduction; also the end-of-backward callback.  Idempotent:
+        once a backward's buckets are joined, another call is a no-op until the next
+        backward fires a grad hook (the demo calls it again after ``backward()``)."""
+        if not self._fired and not self._pending:
+            return
+        if self._fired:
+            for i in range(len(self.params)):  # stages that produced no gradient this backward
+                if i not in self._done:
+                    self._done.add(i)
+                    self._reduce(i)
         for w, i in self._pending:
             p = self.params[i]
             if w == "xgmi":
@@ -282,10 +289,13 @@ class LayerSplitDDP:
         self._pending = []
         self._done = set()
         self._queued = False
+        self._fired = False
 
-    # the reference calls optimizer.step() right after backward: kept as an explicit
-    # join for callers that drive the buckets themselves
-    allreduce_grads = finish
+    def allreduce_grads(self):
+        """Reduce every stage's current ``.grad`` now, for callers that fill gradients
+        without autograd (no grad hook fires); after a backward it only joins."""
+        self._fired = True
+        self.finish()
 
     def check_comm(self):
         for ar in self._xgmi.values():
@@ -438,7 +448,10 @@ class FusedLayerSplit:
             return
         import ctypes
 
-        for ring in self.rings.values():
+        for dev, ring in self.rings.items():
+            # the ring refill is a copy on dev's current stream: order it after the previous
+            # launch on the split stream, which may still read the slots it overwrites
+            torch.cuda.current_stream(dev).wait_stream(self.streams[dev])
             ring.ensure(*ring.epochs_of_steps(self.t, self.t + n_steps - 1))
         for dev, L in self._launch.items():
             st = self.streams[dev]
@@ -503,7 +516,14 @@ class FusedLayerSplit:
                 "v": torch.cat([v.cpu() for v in self.v]), "step": int(self.step[0].item()), "t": self.t}
 
     def load_state_dict(self, sd: dict) -> None:
+        """Restore a checkpoint.  The link and data-parallel granules are tagged with the
+        step number, so rewinding an engine that already trained past the checkpoint
+        would let its receive buffers hand stale granules of later steps to the replay:
+        that is refused (load into a freshly built engine instead)."""
         self._join()
+        if int(sd["t"]) < self.t:
+            raise RuntimeError(f"cannot rewind a layer-split engine from step {self.t} to {int(sd['t'])}: its "
+                               "receive buffers hold granules of later steps; load into a fresh FusedLayerSplit")
         o = 0
         for s, p in enumerate(self.params):
             n = p.numel()

@@ -191,8 +191,8 @@ class Trainer:
         self.precision = precision
         self.gpus = gpus
         self.num_nodes = num_nodes
-        self.max_steps = max_steps
-        self.max_epochs = max_epochs if max_epochs is not None else (1000 if max_steps < 0 else None)
+        self.max_steps = -1 if max_steps is None else int(max_steps)  # PL 1.5: None = unbounded
+        self.max_epochs = max_epochs if max_epochs is not None else (1000 if self.max_steps < 0 else None)
         self.accelerator = accelerator or ("gpu" if torch.cuda.is_available() and gpus else "cpu")
         self.strategy = strategy
         self.log_every_n_steps = max(1, int(log_every_n_steps))  # reference passes 0.03125
@@ -304,7 +304,8 @@ class Trainer:
         # steady-state clock: from the end of batch _STEADY_AFTER on (warm-up batches,
         # graph capture and first kernel loads excluded); synchronised at both ends
         self.steady_time, self.steady_steps, steady_t0, steady_from = None, 0, None, self.global_step + _STEADY_AFTER
-        done = 0 < self.max_steps <= self.global_step
+        done = 0 <= self.max_steps <= self.global_step or \
+            (self.max_epochs is not None and self.current_epoch >= self.max_epochs)
         try:
             while not done:
                 if hasattr(loader, "set_epoch"):
@@ -356,7 +357,7 @@ class Trainer:
                     if self.every_n_train_steps and self.global_step % self.every_n_train_steps == 0:
                         metrics.flush()
                         self._save(model, opts, "last.ckpt")
-                    if 0 < self.max_steps <= self.global_step:
+                    if 0 <= self.max_steps <= self.global_step:
                         done = True
                         break
                 else:
@@ -460,7 +461,12 @@ class Trainer:
             self._import_fused_state(tr, models, opts, self.global_step)
         self.engine_used = "fused"
         spe = geom.steps_per_epoch
-        total = self.max_steps if self.max_steps > 0 else self.max_epochs * spe
+        # the same stopping rule as the module loop: whichever of max_steps / max_epochs
+        # comes first (max_epochs defaults to 1000 when max_steps is unset, __init__)
+        limits = [self.max_steps] if self.max_steps >= 0 else []
+        if self.max_epochs is not None:
+            limits.append(self.max_epochs * spe)
+        total = min(limits)
         logger = CSVLogger(self.root, self.global_rank)
         self._log_dir = logger.dir
         model.on_train_start()
@@ -546,7 +552,14 @@ class Trainer:
                 if all(s.get(key) is not None for s in st):
                     dst.copy_(torch.cat([s[key].reshape(-1).to(dst) for s in st]))
             steps = [s["step"] for s in st if "step" in s]
-            tr.step_ctr[i] = int(float(steps[0])) if steps else global_step
+            step = int(float(steps[0])) if steps else global_step
+            # the persistent engine positions its sampler AND its Adam bias corrections from
+            # one step number (host_t0 = tr.t): a restored optimizer that stepped a different
+            # number of times than the batches that ran cannot continue bit-exactly there
+            if step != global_step:
+                raise RuntimeError(f"resumed optimizer {i} has step {step} but global_step is {global_step}: the fused "
+                                   "engine needs one optimizer step per batch (use engine='module')")
+            tr.step_ctr[i] = step
         tr.t = global_step
 
     @staticmethod

@@ -23,9 +23,12 @@ NAMES = ["step_start", "x_loaded", "fwd+loss", "bwd_done(w0)", "tiles_reduced", 
 
 
 def main():
+    # python scripts/prof_stamps.py [--lanes L --batch B]: L = 2 / 4 stamps the several-lanes step
+    lanes = int(sys.argv[sys.argv.index("--lanes") + 1]) if "--lanes" in sys.argv else 1
+    batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 256
     dev = torch.device("cuda", 0)
     X, Y = ToyData(seed=0).device_tensors(dev)
-    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=256), cfg=EngineConfig())
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=batch), cfg=EngineConfig())
     tr.train(50)  # warm
     tr.synchronize()
     lib = nat.load()
@@ -34,7 +37,10 @@ def main():
     for rep in range(3):
         a = tr._train_args(8, nat.MODE_ADAM, None)
         a.status = nat.ptr(prof)
-        nat.check(lib.dtp_mlp_train_profile(ctypes.byref(a), nat.stream_ptr()), "profile")
+        if lanes > 1:
+            nat.check(lib.dtp_mlp_train_profile_lanes(ctypes.byref(a), lanes, nat.stream_ptr()), "profile")
+        else:
+            nat.check(lib.dtp_mlp_train_profile(ctypes.byref(a), nat.stream_ptr()), "profile")
         torch.cuda.synchronize()
         st = prof.view(2, 8, 32).cpu()
         rows = []
@@ -71,7 +77,8 @@ def main():
     tr.train(2000)
     ev1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"persistent_us_per_step": ev0.elapsed_time(ev1) * 1e3 / 2000}))
+    print(json.dumps({"persistent_us_per_step": ev0.elapsed_time(ev1) * 1e3 / 2000, "engine_lanes": tr.lanes,
+                      "batch": batch}))
 
 
 if __name__ == "__main__":

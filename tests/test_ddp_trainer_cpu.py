@@ -225,3 +225,22 @@ def test_csv_logger_block_rows_match_single_rows(tmp_path):
     b.log_rows(steps[2:], names, rows[2:])
     b.close()
     assert (a.dir / "metrics.csv").read_text() == (b.dir / "metrics.csv").read_text()
+
+
+def test_trainer_stops_at_the_first_of_max_steps_and_max_epochs(tmp_path):
+    """max_epochs bounds the fit when it comes before max_steps (4 batches per epoch), and
+    max_steps=0 runs no batch; the fused engine computes its step total by the same rule
+    (trainer.py:_fit_fused)."""
+    sys.path.insert(0, str(ROOT))
+    from demo_pytorch_lightning import LitToyModel
+    from distributed_training_pytorch_amd.data.toy_data import ToyData
+    from distributed_training_pytorch_amd.trainer import Trainer
+
+    for kw, want in [(dict(max_steps=100, max_epochs=2), 8), (dict(max_steps=3, max_epochs=2), 3),
+                     (dict(max_steps=0), 0), (dict(max_steps=None, max_epochs=1), 4)]:
+        torch.manual_seed(0)
+        dl = torch.utils.data.DataLoader(ToyData(seed=0), batch_size=128)
+        tr = Trainer(gpus=0, accelerator="cpu", log_every_n_steps=1, default_root_dir=str(tmp_path / str(want)),
+                     enable_progress_bar=False, **kw)
+        tr.fit(LitToyModel(), dl)
+        assert tr.global_step == want, (kw, tr.global_step)

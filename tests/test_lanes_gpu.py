@@ -1,0 +1,134 @@
+"""The several-lanes-per-sample fused step (csrc/mlp_lanes.h) against plain autograd +
+torch.optim.Adam, its selection by the per-rank batch, and its self-consistency across
+launch modes (GPU only)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry
+from distributed_training_pytorch_amd.data.toy_data import ToyData
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, MlpSpec
+from distributed_training_pytorch_amd.ops.optim import OptimConfig
+
+from .ref_train import torch_train
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _init(spec, seed, n=2, scale=0.4):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.randn(spec.P, generator=g) * scale).to(DEV) for _ in range(n)]
+
+
+@pytest.mark.parametrize("batch,lanes", [(64, 4), (50, 4), (128, 2), (100, 2), (256, 1)])
+def test_lanes_selected_by_batch_and_match_torch(batch, lanes):
+    """batch 50 / 100: the epoch's last batch is short (512 = 10 x 50 + 12, 5 x 100 + 12),
+    so the lanes past it must drop out of the loss, the dW tiles and the mean."""
+    X, Y = ToyData(n=512, seed=21).device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=3)
+    init = _init(TOY_SPEC, batch)
+    ocfg = OptimConfig(lr=1e-2)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=7), init_params=init)
+    assert tr.lanes == lanes
+    steps = 2 * geom.steps_per_epoch + 3
+    tr.train(steps)
+    tr.synchronize()
+    ref_p, ref_l = torch_train(TOY_SPEC, init, X, Y, [EpochIndexStream(geom)], steps, ocfg)
+    torch.testing.assert_close(tr.losses(0, steps), ref_l, rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(tr.params.cpu(), ref_p, rtol=1e-3, atol=2e-5)
+    assert tr.step_ctr.tolist() == [steps, steps]
+    tr.close()
+
+
+@pytest.mark.parametrize("spec", [MlpSpec(2, 10, 3, 1), MlpSpec(2, 15, 5, 1), MlpSpec(2, 10, 5, 4)],
+                         ids=["nl3", "h15", "out4"])
+@pytest.mark.parametrize("batch", [64, 128])
+def test_lanes_other_shapes_match_torch(spec, batch):
+    """H = 15 leaves a padding slot in the last part (L = 4: 4 x 4 = 16 units; L = 2:
+    2 x 8) that must never reach the tiles; OUT = 4 is a whole last layer of 4 rows."""
+    X, Y = ToyData(n=512, seed=5).device_tensors(DEV)
+    if spec.out_features > 1:
+        Y = torch.randn(512, spec.out_features, device=DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=9)
+    init = _init(spec, 7 + batch, scale=0.3)
+    ocfg = OptimConfig(lr=5e-3)
+    tr = FusedTrainer(spec, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=5), init_params=init)
+    assert tr.lanes == (4 if batch == 64 else 2)
+    steps = 12
+    tr.train(steps)
+    tr.synchronize()
+    ref_p, ref_l = torch_train(spec, init, X, Y, [EpochIndexStream(geom)], steps, ocfg)
+    torch.testing.assert_close(tr.losses(0, steps), ref_l, rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(tr.params.cpu(), ref_p, rtol=1e-3, atol=2e-5)
+    tr.close()
+
+
+@pytest.mark.parametrize("batch", [64, 128])
+def test_lanes_bitwise_across_launch_modes(batch):
+    """The lanes instance is deterministic: one persistent launch, short persistent
+    launches, per-step eager launches and hipGraph replays give bitwise the same run,
+    including a launch longer than the kernel's Adam-scalar table (1024 steps)."""
+    X, Y = ToyData(n=512, seed=2).device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=1)
+    init = _init(TOY_SPEC, 40)
+    res = {}
+    for name, ecfg, steps in [("long", EngineConfig(steps_per_launch=1100), 1100),
+                              ("short", EngineConfig(steps_per_launch=100), 1100),
+                              ("one", EngineConfig(steps_per_launch=1100), 30),
+                              ("eager", EngineConfig(launch="eager"), 30),
+                              ("graph", EngineConfig(launch="graph", steps_per_launch=8), 30)]:
+        tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
+        assert tr.lanes == (4 if batch == 64 else 2)
+        tr.train(steps)
+        tr.synchronize()
+        res[name] = (tr.params.clone(), tr.losses(0, steps))
+        tr.close()
+    assert torch.equal(res["long"][0], res["short"][0]) and torch.equal(res["long"][1], res["short"][1])
+    for k in ("eager", "graph"):
+        assert torch.equal(res["one"][0], res[k][0]), k
+        assert torch.equal(res["one"][1], res[k][1]), k
+
+
+_FORCE_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.toy_data import ToyData
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
+from distributed_training_pytorch_amd.ops.optim import OptimConfig
+dev = torch.device("cuda", 0)
+X, Y = ToyData(n=512, seed=8).device_tensors(dev)
+g = torch.Generator().manual_seed(0)
+init = [(torch.randn(TOY_SPEC.P, generator=g) * 0.4).to(dev) for _ in range(2)]
+tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch={batch}, seed=4), OptimConfig(lr=1e-2),
+                  EngineConfig(steps_per_launch=9), init_params=init)
+lanes = tr.lanes
+tr.train(40)
+tr.synchronize()
+torch.save({{"p": tr.params.cpu(), "l": tr.losses(0, 40), "lanes": lanes}}, {out!r})
+"""
+
+
+def test_lanes_agree_with_one_lane_kernel(tmp_path):
+    """DTP_LANES forces the instance: at batch 64 the L = 1, 2, 4 kernels run the same
+    training (forward / input-gradient chains are the same fmaf sequence; the batch sums
+    are grouped differently, so agreement is to float reassociation)."""
+    outs = {}
+    for flag in ("1", "2", "4"):
+        out = str(tmp_path / f"l{flag}.pt")
+        env = dict(os.environ, DTP_LANES=flag)
+        r = subprocess.run([sys.executable, "-c", _FORCE_SCRIPT.format(root=ROOT, batch=64, out=out)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[flag] = torch.load(out, weights_only=True)
+        assert outs[flag]["lanes"] == int(flag)
+    for flag in ("2", "4"):
+        torch.testing.assert_close(outs[flag]["l"], outs["1"]["l"], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(outs[flag]["p"], outs["1"]["p"], rtol=1e-4, atol=1e-6)

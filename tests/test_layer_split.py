@@ -63,16 +63,19 @@ def _hybrid_rank(rank, world, steps):
     ref = ToyModel()
     ls = LayerSplitMLP(ref.spec, [torch.device("cpu")] * 2, None, 1, ref.flat_params.detach() * (1 + rank))
     ddp = LayerSplitDDP(ls)  # broadcast: rank 1's different init is replaced by rank 0's
+    calls = []
+    reduce_ = ddp._reduce
+    ddp._reduce = lambda i: (calls.append(i), reduce_(i))  # count the bucket reductions
     opts = [FlatOptimizer(p.data, p.grad, OptimConfig(lr=1e-2)) for p in ls.params]
     g = torch.Generator().manual_seed(rank)
     for _ in range(steps):
         x, y = torch.randn(64, 2, generator=g), torch.randn(64, 1, generator=g)
         ls.zero_grad()
         torch.nn.functional.mse_loss(ls(x), y).backward()
-        ddp.finish()
+        ddp.finish()  # the end-of-backward callback already joined: must be a no-op
         for o in opts:
             o.step()
-    return ls.flat_params_cpu(), ddp.comm
+    return ls.flat_params_cpu(), ddp.comm, sorted(calls)
 
 
 def test_hybrid_split_ddp_per_device_buckets_cpu():
@@ -82,6 +85,8 @@ def test_hybrid_split_ddp_per_device_buckets_cpu():
     res = run_ranks(_hybrid_rank, 2, (steps,))
     assert res[0][1] == "gloo"
     assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
+    # one all-reduce per stage bucket per step (a second finish() must not reduce again)
+    assert res[0][2] == sorted([0, 1] * steps), res[0][2]
     # reference: one process, gradient = mean of the two ranks' batch gradients
     torch.manual_seed(0)
     ref = ToyModel()
