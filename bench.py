@@ -165,6 +165,9 @@ def main():
         k = (a.warmup - done) // (split - i)
         train(k)
         done += k
+    xstats = a.impl == "native" and world > 1 and runner.comm == "xgmi"
+    if xstats:
+        runner.exchange_stats_reset()  # stream-ordered, covered by the synchronize below
     sync_barrier()
     sync()
     t0 = time.perf_counter()
@@ -175,6 +178,17 @@ def main():
     ms_per_step = 1e3 * elapsed / a.steps
     total_samples = comm_util.all_reduce_scalar(float(per_rank_batch * a.steps))
     value = total_samples / elapsed
+    diag = {}
+    if world > 1 and a.impl == "native":
+        # where a multi-GPU step goes (readable from the JSON line alone): the in-kernel
+        # exchange's wait (publish -> last peer granule, per rank) and the rest of the step
+        diag["comm_fallback_reason"] = runner.comm_fallback_reason
+        if xstats:
+            w_us, n_ex = runner.exchange_stats()
+            waits = comm_util.all_gather_scalar(w_us / max(1, n_ex))
+            diag["exchange_wait_us_per_step"] = max(waits)
+            diag["exchange_wait_us_per_step_by_rank"] = [round(v, 3) for v in waits]
+            diag["compute_us_per_step"] = 1e3 * ms_per_step - max(waits)
 
     final_loss = None
     if dbar is not None:
@@ -215,6 +229,7 @@ def main():
                 **cfg_desc,
             },
             "final_loss": final_loss,
+            **diag,
         }
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():

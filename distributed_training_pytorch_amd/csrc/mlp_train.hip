@@ -173,6 +173,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     fidx = fast_index(e2, b2);
   }
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
+  unsigned long long xwait = 0;  // exchange-wait ticks of this thread (diagnostic, xgmi_record_wait)
   for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   if (cached) {
     for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       // all-reduce (sum) this model's gradient + loss over every rank through
       // the peers' xGMI-mapped receive buffers, inside the step (xgmi_core.h)
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid);
+      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, &xwait);
     }
 
     // advance the sampler / loss-ring position and gather the next step's first
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     }
     if (tid == 0) a.step[model] = t0 + a.n_steps;
     if (kXgmi && tid == 0) a.epoch[model] = xepoch;
+    if (kXgmi && tid == 0 && model == 0) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps);
     stamp_launch(21);
   }
 }
@@ -568,6 +570,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
   roll(e2, b2);
   int fidx = fast_index(e2, b2);
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
+  unsigned long long xwait = 0;
   for (int e = tid; e < C::pad4(C::LW); e += kBlock) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
   for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * S::IN + e] = a.Y[e];
@@ -808,7 +811,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
     float gloss = mean_loss;
     if constexpr (kXgmi) {
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid);
+      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, &xwait);
     }
     const int lslot_now = lslot;
     roll(epoch, bi);
@@ -853,6 +856,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
   }
   if (tid == 0) a.step[model] = t0 + a.n_steps;
   if (kXgmi && tid == 0) a.epoch[model] = xepoch;
+  if (kXgmi && tid == 0 && model == 0) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps);
 }
 
 // ------------------------------------------------------------------------------

@@ -97,9 +97,12 @@ struct XgmiCtx {
   int world, rank, n_models, timeout_us;
 };
 
+// waited (nullable): += s_memrealtime ticks (100 MHz) from this thread's last publish
+// store to its last granule accepted -- the exchange-wait diagnostic of the bench
+// (status words [4..8), written back once per launch by the caller)
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g)[NPT], float loss, unsigned epoch,
-                                   int tid) {
+                                   int tid, unsigned long long* waited = nullptr) {
   constexpr int GPT = xgmi_gpt<NPT>();
   const int W = a.world, R = a.rank;
   const int slot = xgmi_slot16(P, NPT);
@@ -134,8 +137,8 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   // consume every peer's granules from our local buffer: all pending ones requested
   // at once, only the missing ones re-polled; bounded by the deadline
   const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[R]);
-  const unsigned long long deadline =
-      __builtin_amdgcn_s_memrealtime() + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
+  const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long deadline = t_pub + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
   bool dead = a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
   float val[kXgmiMaxWorld][GPT + 1][2];
   static_assert(kXgmiMaxWorld * (GPT + 1) <= 64, "pending mask holds every (rank, granule) pair");
@@ -226,6 +229,7 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
     __builtin_amdgcn_s_sleep(1);
   }
 #endif
+  if (waited) *waited += __builtin_amdgcn_s_memrealtime() - t_pub;
   // sum in rank order 0..W-1 (bitwise identical on every rank; absent ranks add +0)
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -242,9 +246,18 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
 
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
-                                   unsigned epoch, int tid) {
+                                   unsigned epoch, int tid, unsigned long long* waited = nullptr) {
   const XgmiCtx c{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
-  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid);
+  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid, waited);
+}
+
+// the fused step's exchange diagnostics in the status block: [4..6) u64 wait ticks and
+// [6..8) u64 exchanges of thread 0 of model 0, accumulated over launches (the host
+// zeroes them around a timed region)
+DTP_DEV void xgmi_record_wait(int* status, unsigned long long ticks, unsigned long long n) {
+  if (!status) return;
+  atomicAdd(reinterpret_cast<unsigned long long*>(status + 4), ticks);
+  atomicAdd(reinterpret_cast<unsigned long long*>(status + 6), n);
 }
 
 }  // namespace dtp

@@ -94,6 +94,7 @@ class FusedTrainer:
             torch.cuda.current_device() if self.device.type == "cuda" else -1)
         self._xgmi = None
         self._ring = None
+        self.comm_fallback_reason: str | None = None  # why an xGMI setup fell back to RCCL
         self.comm = self._resolve_comm()
         # DDP construction semantics: every rank starts from rank 0's weights
         if self.world > 1:
@@ -173,8 +174,9 @@ class FusedTrainer:
             ok, why = self._xgmi_selftest()
             ok = self._agree(ok)
         if not ok:
+            self.comm_fallback_reason = why or "a peer failed the xGMI setup or self-test"
             if self.rank == 0:
-                print(f"[dtp] xGMI exchange unavailable ({why or 'a peer failed'}); using RCCL", flush=True)
+                print(f"[dtp] xGMI exchange unavailable ({self.comm_fallback_reason}); using RCCL", flush=True)
             if self._xgmi is not None:
                 if dist.is_initialized():
                     comm_util.barrier(self.group)
@@ -446,6 +448,40 @@ class FusedTrainer:
             torch.cuda.synchronize(self.device)
         if self._xgmi is not None:
             self._xgmi.check_status()
+
+    def step_indices(self, t: int) -> list[int]:
+        """Dataset indices of this rank's batch at step t (the order the kernels read)."""
+        return self._idx_stream.indices(t) if self.cfg.sampler == "torch" else self.geom.indices(t)
+
+    def local_gradients(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """This rank's gradient [n_models, P] and mean loss [n_models] of the NEXT step
+        (step ``t``'s batch, current weights), from the fused kernel's gradient-only launch
+        (MODE_GRAD): no parameter, moment or step counter changes."""
+        if not self.native:
+            raise RuntimeError("local_gradients needs the native engine")
+        self._ensure_epochs(1)
+        lib = nat.load()
+        a = self._train_args(1, nat.MODE_GRAD, None)
+        a.host_t0 = self.t
+        nat.check(lib.dtp_mlp_train(ctypes.byref(a), *self.spec.key[:4], nat.MODE_GRAD, nat.stream_ptr()),
+                  "dtp_mlp_train(grad)")
+        P, n = self.spec.P, self.n_models
+        buf = self.comm_buf.clone()
+        return buf[:n * P].view(n, P), buf[n * P:n * P + n]
+
+    def exchange_stats_reset(self) -> None:
+        """Zero the in-kernel exchange's wait counters (status words [4..8), stream-ordered)."""
+        if self._xgmi is not None:
+            self._xgmi.status[4:8].zero_()
+
+    def exchange_stats(self) -> tuple[float, int] | None:
+        """(microseconds thread 0 of model 0 spent between publishing its gradient granules
+        and accepting the last peer granule, summed over the exchanges since the last
+        reset; number of exchanges) -- None without the in-kernel xGMI exchange.  Syncs."""
+        if self._xgmi is None:
+            return None
+        w = self._xgmi.status[4:8].cpu().view(torch.int64).tolist()
+        return w[0] / 100.0, int(w[1])  # s_memrealtime runs at 100 MHz
 
     def check_comm(self):
         """Raise if the in-kernel exchange hit its (sticky) timeout. One small read;

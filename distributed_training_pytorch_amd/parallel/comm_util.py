@@ -60,3 +60,12 @@ def all_reduce_scalar(x: float, op=dist.ReduceOp.SUM, group=None) -> float:
         return float(x)
     t = torch.tensor([float(x)], dtype=torch.float64)
     return float(all_reduce_(t, group, op=op).item())
+
+
+def all_gather_scalar(x: float, group=None) -> list[float]:
+    """Every rank's host float, in rank order (one SUM all-reduce of a one-hot f64 vector)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [float(x)]
+    t = torch.zeros(dist.get_world_size(group), dtype=torch.float64)
+    t[dist.get_rank(group)] = float(x)
+    return [float(v) for v in all_reduce_(t, group).tolist()]

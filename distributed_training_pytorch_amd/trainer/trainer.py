@@ -23,6 +23,7 @@ from __future__ import annotations
 import contextlib
 import csv
 import datetime
+import math
 import os
 import time
 from pathlib import Path
@@ -219,6 +220,7 @@ class Trainer:
             raise ValueError(f"engine={engine!r}: auto, fused or module")
         self.engine = engine
         self.engine_used = "module"
+        self.fused_refused: str | None = None  # why fused_spec() was not trusted (checked on the first batch)
         self._skip_batches = 0
         self._batch_in_epoch = 0
         self._log_dir = None
@@ -277,7 +279,9 @@ class Trainer:
             self._restore(model, opts, resume)
         plan = self._fused_plan(model, opts, dl)
         if plan is not None:
-            return self._fit_fused(model, opts, plan)
+            done = self._fit_fused(model, opts, plan)
+            if done is not None:
+                return done
         # the flat gradient buffer of FlatDDP also serves one process: fused kernels add
         # their parameter gradients into its views in place (no AccumulateGrad adds)
         single_ok = self.device.type == "cuda" and all(
@@ -459,6 +463,17 @@ class Trainer:
         self._skip_batches = 0  # the engine positions its sampler from the step count
         if self.global_step:  # resumed: the torch optimizers' state continues in the engine
             self._import_fused_state(tr, models, opts, self.global_step)
+        # fused_spec() is a declaration: check it against training_step on the first batch
+        # before the engine trains anything (every rank agrees on the outcome)
+        why = self._verify_fused_spec(model, opts, plan, tr, X, Y)
+        if why is not None:
+            tr.close()
+            if self.engine == "fused":
+                raise RuntimeError(f"Trainer(engine='fused'): {why}")
+            if self.global_rank == 0:
+                rank_print(0, f"Trainer: not using the fused engine ({why}); per-batch module path")
+            self.fused_refused = why
+            return None
         self.engine_used = "fused"
         spe = geom.steps_per_epoch
         # the same stopping rule as the module loop: whichever of max_steps / max_epochs
@@ -539,6 +554,58 @@ class Trainer:
             self._save(model, opts, final)
         logger.close()
         return self
+
+    def _verify_fused_spec(self, model, opts, plan, tr, X, Y) -> str | None:
+        """Run ``training_step`` once on the batch the engine trains first (module path,
+        autograd, no optimizer step) and compare every model's logged loss and parameter
+        gradient with the engine's gradient-only launch of the same step (MODE_GRAD:
+        local means, nothing updated).  Returns None when they agree (rtol 1e-4, atol
+        1e-5: fp32 under different summation orders), else the reason.  All ranks take
+        the same decision."""
+        models, names = plan["models"], plan["names"]
+        why = None
+        try:
+            idx = torch.as_tensor(tr.step_indices(self.global_step), dtype=torch.long, device=X.device)
+            batch = [X[idx], Y[idx]]
+            eng_g, eng_l = tr.local_gradients()
+            saved = [p.requires_grad for p in model.parameters()]
+            try:
+                for oi, m in enumerate(models):
+                    if len(opts) > 1:
+                        model.toggle_optimizer(opts[oi], oi, opts)
+                    with self._autocast():
+                        out = model.training_step(batch, 0, oi) if len(opts) > 1 else model.training_step(batch, 0)
+                    loss = out["loss"] if isinstance(out, dict) else out
+                    ps = list(m.parameters())
+                    gs = torch.autograd.grad(loss, ps, allow_unused=True)
+                    g = torch.cat([(torch.zeros_like(p) if q is None else q).reshape(-1) for p, q in zip(ps, gs)])
+                    logged = model._logged.get(names[oi])
+                    if len(opts) > 1:
+                        model.untoggle_optimizer(oi)
+                    if logged is None:
+                        why = f"training_step does not log {names[oi]!r}"
+                        break
+                    lv = float(torch.as_tensor(logged).detach().float().reshape(-1)[0])
+                    tol = 1e-2 if plan["precision"] == "bf16" else 1e-4
+                    if not math.isclose(lv, float(eng_l[oi]), rel_tol=tol, abs_tol=1e-5):
+                        why = f"{names[oi]} of training_step is {lv:.6g}, the declared step gives {float(eng_l[oi]):.6g}"
+                        break
+                    if not torch.allclose(g.float(), eng_g[oi], rtol=tol, atol=1e-5 if tol < 1e-3 else 1e-3):
+                        err = (g.float() - eng_g[oi]).abs().max().item()
+                        why = f"model {oi}'s gradient from training_step differs from fused_spec's (max err {err:.3g})"
+                        break
+            finally:
+                for p, r in zip(model.parameters(), saved):
+                    p.requires_grad_(r)
+                model._logged.clear()
+        except Exception as e:  # noqa: BLE001 - any failure of the check refuses the engine
+            why = f"fused_spec check failed: {e}"
+        if self.world_size > 1:
+            flag = torch.tensor([0.0 if why is None else 1.0])
+            comm_util.all_reduce_(flag)
+            if why is None and flag.item() > 0:
+                why = "fused_spec check failed on another rank"
+        return why
 
     @staticmethod
     def _import_fused_state(tr, models, opts, global_step: int) -> None:

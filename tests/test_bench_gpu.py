@@ -88,6 +88,13 @@ def test_bench_strong_scaling_share_gpu(world):
     assert rec["config"]["dataset_samples"] == 512
     assert rec["config"]["global_batch"] == 512
     assert rec["config"]["per_rank_batch"] == 512 // world
+    # per-rank batch 256 / 128 / 64: the one-lane step, then the 2- and 4-lanes steps
+    assert rec["config"]["lanes_per_sample"] == {2: 1, 4: 2, 8: 4}[world], rec["config"]
+    # the multi-GPU diagnostics of the line: no fallback, exchange wait and compute split
+    assert rec["comm_fallback_reason"] is None
+    assert len(rec["exchange_wait_us_per_step_by_rank"]) == world
+    assert 0 <= rec["exchange_wait_us_per_step"] <= 1e3 * rec["ms_per_step"]
+    assert rec["compute_us_per_step"] > 0
     ref = _single_process_full_batch_losses(steps + warmup)
     for got, want in zip(rec["final_loss"], ref):
         assert abs(got - want) <= 1e-3 * abs(want) + 1e-5, (rec["final_loss"], ref)
