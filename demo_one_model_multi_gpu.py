@@ -159,10 +159,9 @@ def _run_fused(config, eng, geom, world, rank, logger, faults, pbar) -> dict:
         nonlocal last
         it0, n, handle = p
         ls = handle.wait()
-        for k in range(n):
-            if rank == 0:
-                # the reference logs the local loss (demo_one_model_multi_gpu.py:129-130); this is the global mean
-                logger.log({"loss/loss": ls[k][0]}, step=it0 + k)
+        # one block per launch (the reference logs the local loss every iteration,
+        # demo_one_model_multi_gpu.py:129-130; this is the global mean, same key)
+        logger.log_rows(list(range(it0, it0 + n)), ["loss/loss"], ls[:n])
         if n:
             last = ls[n - 1][0]
         if pbar is not None:

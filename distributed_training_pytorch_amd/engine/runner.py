@@ -187,9 +187,7 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
         it0, n, handle = p
         with timer.phase("loss_readback"):
             ls = handle.wait()  # raises on a sticky xGMI timeout: never train on partial sums
-        for k in range(n):
-            logger.log({"loss/lossX": ls[k][0]}, step=it0 + k, commit=False)
-            logger.log({"loss/lossY": ls[k][1]}, step=it0 + k)
+        logger.log_rows(list(range(it0, it0 + n)), ["loss/lossX", "loss/lossY"], ls[:n])
         if pbar is not None:
             pbar.update(n)
 

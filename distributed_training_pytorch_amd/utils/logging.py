@@ -12,6 +12,7 @@ Only rank 0 logs, as in the reference.
 from __future__ import annotations
 
 import json
+import math
 import os
 import time
 from pathlib import Path
@@ -60,6 +61,26 @@ class MetricLogger:
             self._f.write(json.dumps({"step": step, **{k: float(v) for k, v in metrics.items()}}) + "\n")
         if commit:
             self.step = step + 1
+
+    def log_rows(self, steps: list[int], names: list[str], rows: list[list[float]]) -> None:
+        """A block of per-step metrics in one call (the fused engines read their losses
+        back once per launch): the same rows ``log`` writes -- one wandb row per step
+        with every name, one JSONL line per step -- built as one string and written once."""
+        if not self.enabled or not steps:
+            return
+        if self._wandb is not None:
+            for st, row in zip(steps, rows):
+                self._wandb.log(dict(zip(names, map(float, row))), step=st)
+        if self._f is not None:
+            keys = [json.dumps(n) for n in names]
+
+            def num(v):  # json.dumps' spelling (repr for finite floats, NaN / Infinity otherwise)
+                v = float(v)
+                return repr(v) if math.isfinite(v) else json.dumps(v)
+
+            self._f.write("".join('{"step": %d, %s}\n' % (st, ", ".join("%s: %s" % (k, num(v)) for k, v in zip(keys, row)))
+                                  for st, row in zip(steps, rows)))
+        self.step = steps[-1] + 1
 
     def finish(self) -> None:
         if not self.enabled:
