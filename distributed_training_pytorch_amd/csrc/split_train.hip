@@ -87,14 +87,19 @@ DTP_DEV void link_recv(const void* buf, int slot, unsigned ep, float (&v)[16], b
   }
 }
 
+// Adam bias-correction scalars of the next kSplitAdamTab steps, formed once per that
+// many steps in f64 (torch's host math) -- not per step
+constexpr int kSplitAdamTab = 1024;
+
 template <class S>
 struct SplitSmem {
   float w[S::pad4(S::LP)];        // weights, row-major + transposed copies (mlp_core.h)
   float stage[kBlock / kWave][2 * kStgArr];  // per-wave dW staging, reused for the cross-wave reduction
   float data[kSplitCache];
+  float2 adam_tab[kSplitAdamTab];  // {lr / (1 - b1^t), sqrt(1 - b2^t)} of steps t0 + base + e + 1
 };
 
-constexpr int kSplitSmemBytes = 72 * 1024;  // the largest stage's SplitSmem
+constexpr int kSplitSmemBytes = 80 * 1024;  // the largest stage's SplitSmem
 
 // One pipeline stage, n_steps iterations.  FIRST: gathers the batch inputs from the
 // dataset; LAST: gathers the targets and computes the MSE loss; otherwise the
@@ -137,6 +142,35 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
       for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * XW + e] = a.Y[e];
   }
   const int t0 = a.step[0];
+  // sampler cursor (epoch, batch of the epoch), advanced incrementally: no 64-bit
+  // division per step
+  int epoch = t0 / smp.steps_per_epoch;
+  int bi = t0 - epoch * smp.steps_per_epoch;
+  // the dataset index of this lane's sample at cursor (ep, b) -- requested a step ahead
+  // (the ring / Feistel lookup overlaps the previous step's reduction and optimizer)
+  auto index_at = [&](int ep, int b) -> int {
+    if constexpr (!(FIRST || LAST)) {
+      return 0;
+    } else {
+      BatchPos bp;
+      bp.epoch = ep;
+      bp.start = b * smp.batch;
+      bp.size = min(smp.batch, smp.num_samples - bp.start);
+      uint32_t keys[4];
+      epoch_keys(smp, ep, keys);
+      return tid < bp.size ? sample_index(smp, bp, keys, tid) : 0;
+    }
+  };
+  int di_next = index_at(epoch, bi);
+  auto fill_adam = [&](int base) {
+    const int n = min(kSplitAdamTab, a.n_steps - base);
+    for (int e = tid; e < n; e += kBlock) {
+      const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
+      const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
+      sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
+    }
+  };
+  if (adam) fill_adam(0);
   __syncthreads();  // pads zeroed before the owners scatter
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -153,15 +187,15 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
   for (int it = 0; it < a.n_steps; ++it) {
     const int t = t0 + it;
     const unsigned ep = (unsigned)t + 1u;
-    const BatchPos bp = batch_pos(smp, t);
-    const int bsz = bp.size;
+    const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
     const bool valid = tid < bsz;
-    int di = 0;
-    if (FIRST || LAST) {
-      uint32_t keys[4];
-      epoch_keys(smp, bp.epoch, keys);
-      di = valid ? sample_index(smp, bp, keys, tid) : 0;
+    const int di = di_next;
+    // the next step's cursor and index request (consumed one step later)
+    if (++bi == smp.steps_per_epoch) {
+      bi = 0;
+      ++epoch;
     }
+    if (it + 1 < a.n_steps) di_next = index_at(epoch, bi);
     // ---- forward
     float h[NL + 1][16];
     if constexpr (FIRST) {
@@ -226,7 +260,10 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
     // ---- optimizer (registers) + weight refresh (LDS)
     const float gs = a.hp.grad_scale;
     if (adam) {
-      const AdamScalars as = adam_scalars(a.hp, (long long)t + 1);
+      AdamScalars as = adam_consts(a.hp);
+      const float2 sc = sm.adam_tab[it % kSplitAdamTab];
+      as.step_size = sc.x;
+      as.bc2_sqrt = sc.y;
 #pragma unroll
       for (int k = 0; k < NPT; ++k)
         if (lp[k] >= 0) adam_update(pw[k], mr[k], vr[k], g[k] * gs, as);
@@ -246,6 +283,10 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
       if (tid == owner && a.loss_log) a.loss_log[t % a.loss_log_cap] = use_dp ? gloss * gs : loss;
     }
     __syncthreads();  // new weights visible; reduction tiles consumed before the next staging writes
+    if (adam && (it + 1) % kSplitAdamTab == 0 && it + 1 < a.n_steps) {
+      fill_adam(it + 1);  // every thread read this step's entry before the barrier above
+      __syncthreads();
+    }
   }
 
 #pragma unroll

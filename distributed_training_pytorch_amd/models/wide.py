@@ -1,9 +1,8 @@
 """WideMLP: the ToyModel architecture (Linear + LeakyReLU stack, ``toy_model_and_data.py:8-25``)
 at widths where the matmuls are real GEMMs -- every Linear runs through ``ops.gemm``:
-the LDS-tiled MFMA GEMM of ``csrc/gemm.hip`` (bias + activation fused into the
-epilogue, activation gradient fused into the input-gradient GEMM) or, for the large
-bf16 layer problems, hipBLASLt plus one in-place epilogue pass (``DTP_GEMM_BACKEND``);
-fp32 or bf16 compute.
+the LDS-tiled MFMA GEMMs of ``csrc/gemm.hip`` / ``csrc/gemm_ph8.hip`` (bias +
+activation fused into the epilogue, activation gradient fused into the input-gradient
+GEMM); fp32 or bf16 compute.
 
 Same ``layers.{2i}.{weight,bias}`` state-dict layout as ``ToyModel``; parameters
 are views into one flat fp32 buffer, so ``FlatDDP`` all-reduces them as one

@@ -16,24 +16,17 @@ Replaces the reference's cuBLAS ``addmm``/``mm`` + ATen ``leaky_relu(_backward)`
 On CPU tensors every function runs the PyTorch reference of the same math (the
 gloo test paths); on a GPU the HIP kernels are required.
 
-Backend for large bf16 problems (``DTP_GEMM_BACKEND`` / ``set_backend``):
-``mfma`` (default) always runs the kernels above -- the 256x256 bf16 layer GEMMs on
-the eight-phase LDS-DMA kernel (``csrc/gemm_ph8.hip``), few-tile long-K problems
-(the weight gradient of a <= 2048-wide layer) on its split-K plan.  Measured end to
-end (``profiles/gemm_r3_ph8/``) it is the fastest of the three on the 1024/2048/4096-
-wide MLPs: 1.30 / 1.81 / 4.64 ms per step vs 1.63 / 1.92 / 4.90 with hipBLASLt and
-2.47 / 2.32 / 5.82 stock.  ``blaslt`` runs the GEMM on hipBLASLt (``torch.mm``/
-``addmm``, fp32 output through ``out_dtype``) with the epilogue as one extra in-place
-elementwise pass -- an A/B reference only; ``auto`` times both once per problem
-signature (scratch outputs, events) and keeps hipBLASLt only when it is at least
-``_TUNE_MARGIN`` faster.  Calls that pin a kernel (``fast`` / ``splitk`` /
-``force_big``), fp32 operands, ``alpha != 1``, K <= 16, N or M == 1 and problems
-under ``_TUNE_MIN_FLOP`` always run the MFMA kernels.
+One backend: the HIP kernels of this library.  The 256x256 bf16 layer GEMMs run on
+the eight-phase LDS-DMA kernel (``csrc/gemm_ph8.hip``), few-tile long-K problems (the
+weight gradient of a <= 2048-wide layer) on its split-K plan.  Measured end to end
+(``profiles/gemm_r3_ph8/``): 1.30 / 1.81 / 4.64 ms per step on the 1024 / 2048 / 4096-
+wide MLPs vs 1.63 / 1.92 / 4.90 with hipBLASLt + an epilogue pass and 2.47 / 2.32 /
+5.82 stock.  The hipBLASLt variant used for that A/B lives outside the library
+(``scripts/blaslt_ref.py``).
 """
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
@@ -41,31 +34,6 @@ from .. import _native as nat
 
 _DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16}
 _BM = 128
-_BACKENDS = ("auto", "mfma", "blaslt")
-_backend = os.environ.get("DTP_GEMM_BACKEND", "mfma")
-if _backend not in _BACKENDS:
-    raise ValueError(f"DTP_GEMM_BACKEND={_backend!r}: expected one of {_BACKENDS}")
-_TUNE_MIN_FLOP = 4e9      # below this the fused kernel (no extra epilogue pass) is kept
-_TUNE_MARGIN = 0.95       # hipBLASLt + epilogue pass must be >= 5 % faster
-_tuned: dict[tuple, str] = {}
-
-
-def set_backend(name: str) -> None:
-    """``blaslt`` | ``mfma`` | ``auto`` for the large bf16 GEMMs (see module doc)."""
-    global _backend
-    if name not in _BACKENDS:
-        raise ValueError(f"gemm backend {name!r}: expected one of {_BACKENDS}")
-    _backend = name
-
-
-def get_backend() -> str:
-    return _backend
-
-
-def tuned_choices() -> dict:
-    """{problem signature: backend} decided so far by ``auto``."""
-    return dict(_tuned)
-
 
 def _ld(t: torch.Tensor, name: str) -> int:
     if t.dim() != 2:
@@ -129,14 +97,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bo
             r = r + out.float()
         out.copy_(r.to(out_dtype))
         return out
-    lib = nat.require(a.device)  # loud on a GPU box without the extension, whichever backend runs
-    pinned = fast is not None or splitk is not None or force_big
-    if (not pinned and _backend != "mfma" and _blaslt_eligible(a, M, N, K, alpha)
-            and not (accumulate and (aux is not None or act))):  # the kernel adds old C after the activation
-        key = (M, N, K, trans_a, trans_b, out_dtype, bias is not None, aux is not None, act, accumulate)
-        if _backend == "blaslt" or _choose(key, a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate,
-                                           out_dtype) == "blaslt":
-            return _gemm_blaslt(a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate, out_dtype)
+    lib = nat.require(a.device)  # loud on a GPU box without the extension
     return _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, out, bias, aux, act, slope, accumulate, alpha,
                         splitk, out_dtype, force_big, fast)
 
@@ -177,70 +138,6 @@ def _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, out, bias, aux, act, slop
         args.splitk = int(splitk if splitk is not None else 1)
     nat.check(lib.dtp_gemm(args, nat.stream_ptr()), "dtp_gemm")
     return out
-
-
-def _blaslt_eligible(a: torch.Tensor, M: int, N: int, K: int, alpha: float) -> bool:
-    return (a.dtype == torch.bfloat16 and alpha == 1.0 and K > 16 and min(M, N) > 1
-            and 2.0 * M * N * K >= _TUNE_MIN_FLOP)
-
-
-def _gemm_blaslt(a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate, out_dtype):
-    """The same contract as the fused kernel, GEMM on hipBLASLt, epilogue in place after it."""
-    A = a.t() if trans_a else a        # [M, K]
-    Bt = b if trans_b else b.t()       # [K, N]
-    lowp = out_dtype == a.dtype
-    if accumulate:
-        if lowp:
-            out.add_(torch.mm(A, Bt))
-        else:
-            torch.addmm(out, A, Bt, out_dtype=out_dtype, out=out)
-        if bias is not None:
-            out.add_(bias)
-    elif bias is not None:
-        if lowp:
-            torch.addmm(bias.to(out_dtype), A, Bt, out=out)
-        else:
-            torch.addmm(bias.float(), A, Bt, out_dtype=out_dtype, out=out)
-    elif lowp:
-        torch.mm(A, Bt, out=out)
-    else:
-        torch.mm(A, Bt, out_dtype=out_dtype, out=out)
-    if aux is not None:  # out *= LeakyReLU'(aux), one pass, in place
-        aux = aux if aux.dtype == out.dtype else aux.to(out.dtype)
-        torch.ops.aten.leaky_relu_backward.grad_input(out, aux, slope, False, grad_input=out)
-    if act:
-        torch.nn.functional.leaky_relu_(out, slope)
-    return out
-
-
-def _event_ms(fn, reps: int = 8) -> float:
-    fn()  # first call: hipBLASLt heuristic lookup / code object load
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps
-
-
-def _choose(key, a, b, trans_a, trans_b, out, bias, aux, act, slope, accumulate, out_dtype) -> str:
-    got = _tuned.get(key)
-    if got is not None:
-        return got
-    if torch.cuda.is_current_stream_capturing():
-        return "mfma"  # no timing inside a graph capture; decided on the next eager call
-    scratch = out.clone()  # the caller's output is never written by the trial runs
-    lib = nat.require(a.device)
-    M, N = out.shape
-    K = a.shape[0] if trans_a else a.shape[1]
-    t_mfma = _event_ms(lambda: _gemm_native(lib, a, b, M, N, K, trans_a, trans_b, scratch, bias, aux, act, slope,
-                                            accumulate, 1.0, None, out_dtype, False, None))
-    t_lt = _event_ms(lambda: _gemm_blaslt(a, b, trans_a, trans_b, scratch, bias, aux, act, slope, accumulate,
-                                          out_dtype))
-    del scratch
-    _tuned[key] = "blaslt" if t_lt < _TUNE_MARGIN * t_mfma else "mfma"
-    return _tuned[key]
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:

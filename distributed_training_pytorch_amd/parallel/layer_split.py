@@ -324,7 +324,8 @@ class FusedLayerSplit:
 
     def __init__(self, spec: MlpSpec, devices: list[torch.device], X: torch.Tensor, Y: torch.Tensor, geom,
                  optim, init_flat: torch.Tensor, boundaries: list[tuple[int, int]] | None = None, group=None,
-                 timeout_us: int = 2_000_000, log_cap: int = 1 << 16, sampler: str = "torch"):
+                 timeout_us: int = 2_000_000, log_cap: int = 1 << 16, sampler: str = "torch",
+                 launch: str = "per_device"):
         import ctypes
 
         from ..ops.optim import OptimConfig
@@ -390,17 +391,35 @@ class FusedLayerSplit:
             kind = "torch" if sampler == "torch" else "feistel"
             for dev in {self.devices[0], self.devices[-1]}:
                 self.rings[dev] = PermutationRing(geom, dev, kind=kind)
-        # the stages that share a GPU run as ONE launch (one workgroup each: co-resident
-        # by construction); one stream per GPU
-        self.groups: dict[torch.device, list[int]] = {}
+        # launch = "per_device": the stages that share a GPU run as ONE launch (one
+        # workgroup each: co-resident by construction), one stream per GPU.
+        # launch = "per_stage": every stage is its own launch on its own stream -- what a
+        # node with one GPU per stage runs anyway; stages that share a GPU then get
+        # streams with DISJOINT CU masks, i.e. separate hardware queues (two persistent
+        # kernels that wait on each other must never sit behind one another in one
+        # in-order queue), which rehearses the multi-GPU launch path on one GPU
+        if launch not in ("per_device", "per_stage"):
+            raise ValueError(f"launch={launch!r}: per_device or per_stage")
+        self.launch_mode = launch
+        self.groups: dict = {}  # launch key -> stage indices (key: device, or stage index)
         for s, dev in enumerate(self.devices):
-            self.groups.setdefault(dev, []).append(s)
+            self.groups.setdefault(dev if launch == "per_device" else s, []).append(s)
         if any(len(v) > nat.SPLIT_MAX_LOCAL for v in self.groups.values()):
             raise ValueError(f"at most {nat.SPLIT_MAX_LOCAL} stages per GPU")
-        self.streams = {dev: torch.cuda.Stream(device=dev) for dev in self.groups}
+        self.key_dev = {k: self.devices[v[0]] for k, v in self.groups.items()}
+        self.streams = {}
+        for k, v in self.groups.items():
+            dev = self.key_dev[k]
+            shared = sum(1 for d in self.devices if d == dev) > 1
+            if launch == "per_stage" and shared:
+                j = [s for s in range(K) if self.devices[s] == dev].index(v[0])
+                self.streams[k] = nat.cu_masked_stream(dev, [2 * j, 2 * j + 1])
+            else:
+                self.streams[k] = torch.cuda.Stream(device=dev)
         self.t = 0
         self._launch = {}
-        for dev, stages in self.groups.items():
+        for key, stages in self.groups.items():
+            dev = self.key_dev[key]
             L = nat.SplitLaunch()
             L.n = len(stages)
             for j, s in enumerate(stages):
@@ -428,7 +447,7 @@ class FusedLayerSplit:
                 a.hp = self.optim.hyper(spec.slope, 1.0 / self.world)
                 L.shape_id[j] = lib.dtp_split_shape_id(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
                                                        int(ss.final_act), int(s == 0))
-            self._launch[dev] = L
+            self._launch[key] = L
         for d in set(self.devices):
             torch.cuda.synchronize(d)
 
@@ -450,11 +469,14 @@ class FusedLayerSplit:
 
         for dev, ring in self.rings.items():
             # the ring refill is a copy on dev's current stream: order it after the previous
-            # launch on the split stream, which may still read the slots it overwrites
-            torch.cuda.current_stream(dev).wait_stream(self.streams[dev])
+            # launches on the split streams, which may still read the slots it overwrites
+            for k, st in self.streams.items():
+                if self.key_dev[k] == dev:
+                    torch.cuda.current_stream(dev).wait_stream(st)
             ring.ensure(*ring.epochs_of_steps(self.t, self.t + n_steps - 1))
-        for dev, L in self._launch.items():
-            st = self.streams[dev]
+        for key, L in self._launch.items():
+            dev = self.key_dev[key]
+            st = self.streams[key]
             st.wait_stream(torch.cuda.current_stream(dev))  # after any host-side state edits
             for j in range(L.n):
                 L.stage[j].n_steps = n_steps
@@ -463,8 +485,8 @@ class FusedLayerSplit:
         self.t += n_steps
 
     def _join(self):
-        for dev, st in self.streams.items():
-            torch.cuda.current_stream(dev).wait_stream(st)
+        for k, st in self.streams.items():
+            torch.cuda.current_stream(self.key_dev[k]).wait_stream(st)
 
     def synchronize(self):
         self._join()
@@ -495,7 +517,9 @@ class FusedLayerSplit:
 
         dev = self.devices[-1]
         cur = torch.cuda.current_stream(dev)
-        cur.wait_stream(self.streams[dev])
+        for k, st in self.streams.items():
+            if self.key_dev[k] == dev:
+                cur.wait_stream(st)
         cap = self.loss_log.shape[0]
         ids = torch.arange(max(t0, t1 - cap), t1) % cap
         with torch.cuda.device(dev):

@@ -102,13 +102,15 @@ def main():
     ap.add_argument("--shadow", action="store_true",
                     help="ours: the Adam kernel writes the bf16 weight operands (ops/gemm.py ComputeShadow) "
                          "instead of a cast before every forward")
-    ap.add_argument("--gemm-backend", choices=["auto", "mfma", "blaslt"], default=None,
-                    help="ops/gemm.py backend for our implementation (default: DTP_GEMM_BACKEND or auto)")
+    ap.add_argument("--gemm-backend", choices=["mfma", "blaslt"], default="mfma",
+                    help="mfma: the library's kernels; blaslt: the large bf16 GEMMs on hipBLASLt + an epilogue "
+                         "pass (scripts/blaslt_ref.py, an A/B reference outside the library)")
     a = ap.parse_args()
-    from distributed_training_pytorch_amd.ops import gemm as gemm_mod
+    if a.gemm_backend == "blaslt":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from blaslt_ref import use_blaslt
 
-    if a.gemm_backend:
-        gemm_mod.set_backend(a.gemm_backend)
+        use_blaslt()
     env = bootstrap.detect()
     rank, world = env.rank, env.world_size
     dev = bootstrap.bind_device(env)
@@ -134,11 +136,8 @@ def main():
                               "world": world, "ms_per_step": 1e3 * dt / a.steps,
                               "samples_per_s": a.batch * world * a.steps / dt, "model_tflops": flops / dt / 1e12,
                               "dtype": "bf16 compute, fp32 master weights",
-                              "gemm_backend": gemm_mod.get_backend() if impl == "ours" else "torch",
-                              "weight_shadow": a.shadow if impl == "ours" else None,
-                              "tuned": {"x".join(map(str, k[:3])) + ("T" if k[3] else "N") + ("T" if k[4] else "N")
-                                        + ("+acc" if k[9] else "") + ("+aux" if k[7] else "") + ("+act" if k[8] else ""):
-                                        v for k, v in gemm_mod.tuned_choices().items()} if impl == "ours" else {}}),
+                              "gemm_backend": a.gemm_backend if impl == "ours" else "torch",
+                              "weight_shadow": a.shadow if impl == "ours" else None}),
                   flush=True)
         del step
         torch.cuda.empty_cache()

@@ -5,6 +5,7 @@ D=${1:-r4a}
 mkdir -p gpurun_out/$D
 bash scripts/gpu_steps.sh \
   "400|$D/lanes_tests|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_lanes_gpu.py tests/test_trainer_fused_gpu.py" \
+  "400|$D/split|python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_split_fused_gpu.py tests/test_layer_split.py" \
   "300|$D/bench_batch|for b in 64 128 256; do python bench.py --scaling weak --batch \$b; done" \
   "200|$D/bench_forced|for l in 1 2 4; do DTP_LANES=\$l python bench.py --scaling weak --batch 64; done" \
   "200|$D/stamps|python scripts/prof_stamps.py --lanes 4 --batch 64 && python scripts/prof_stamps.py --lanes 2 --batch 128" \

@@ -27,10 +27,10 @@ def _init(seed=5):
     return torch.randn(TOY_SPEC.P, generator=torch.Generator().manual_seed(seed)) * 0.4
 
 
-def _engine(K, ocfg, bounds=None, batch=256, world=1, rank=0, seed=11):
+def _engine(K, ocfg, bounds=None, batch=256, world=1, rank=0, seed=11, **kw):
     ds = ToyData(n=512, seed=2)
     geom = SamplerGeometry(n=512, world=world, rank=rank, batch=batch, seed=seed)
-    return FusedLayerSplit(TOY_SPEC, [DEV] * K, ds.X, ds.Y, geom, ocfg, _init(), boundaries=bounds), ds
+    return FusedLayerSplit(TOY_SPEC, [DEV] * K, ds.X, ds.Y, geom, ocfg, _init(), boundaries=bounds, **kw), ds
 
 
 def _reference(ocfg, steps, batch=256, world=1, seed=11):
@@ -109,3 +109,22 @@ def test_fused_split_with_data_parallel_two_ranks():
         torch.testing.assert_close(res[r][1], rl, rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(res[r][0], rp, rtol=1e-4, atol=2e-5)
     assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
+
+
+@pytest.mark.parametrize("K", [2, 3, 5])
+def test_fused_split_per_stage_launches(K):
+    """The launch path of a node with one GPU per stage: every stage its own persistent
+    launch on its own stream (here: CU-masked streams with disjoint masks on the one GPU,
+    so each stage has its own hardware queue).  Same numbers as the unsplit reference,
+    no link timeout."""
+    ocfg = OptimConfig(lr=1e-2)
+    steps = 12
+    eng, _ = _engine(K, ocfg, launch="per_stage", timeout_us=500_000)
+    assert len(eng._launch) == K and eng.launch_mode == "per_stage"
+    eng.train(5)
+    eng.train(steps - 5)
+    eng.synchronize()  # raises on a link / exchange timeout
+    rp, rl = _reference(ocfg, steps)
+    torch.testing.assert_close(eng.losses(0, steps), rl, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(eng.flat_params_cpu(), rp, rtol=1e-4, atol=2e-5)
+    eng.close()
