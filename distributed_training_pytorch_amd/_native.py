@@ -88,6 +88,9 @@ class TrainArgs(ctypes.Structure):
         ("host_t0", c_int),
         ("smp", SamplerCfg),
         ("hp", Hyper),
+        ("adam_tab", c_void_p),
+        ("adam_tab_len", c_int),
+        ("pad2_", c_int),
     ]
 
 

@@ -47,6 +47,12 @@ struct DtpTrainArgs {
   int host_t0;          // >= 0: the step number of the first step (= the device counters), else read them
   dtp::SamplerCfg smp;
   DtpHyper hp;
+  // Adam bias-correction scalars {lr / (1 - b1^t), sqrt(1 - b2^t)} of step t at [t], formed on
+  // the host in f64 (torch's math); [len - 1] holds the saturated values (every later t).
+  // Nullable: the kernel forms them itself.  Used with host_t0 >= 0 (the persistent engine).
+  const float* adam_tab;  // [adam_tab_len][2]
+  int adam_tab_len;
+  int pad2_;
 };
 
 int dtp_version(void);

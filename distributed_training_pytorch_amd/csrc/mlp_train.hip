@@ -35,6 +35,25 @@ constexpr int kAdamTab = 1024;
 
 constexpr int kWaves = kBlock / kWave;
 
+// entries base + tid + j * kBlock (j < J) of the host's Adam table for a launch starting
+// at step t0: {lr / (1 - b1^t1), sqrt(1 - b2^t1)} with t1 = t0 + e + 1, clamped to the
+// table's saturated last row
+template <int J>
+DTP_DEV void adam_tab_load(const DtpTrainArgs& a, int t0, int base, int tid, float2 (&v)[J]) {
+  const float2* __restrict__ tab = reinterpret_cast<const float2*>(a.adam_tab);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const long long t1 = (long long)t0 + base + tid + j * kBlock + 1;
+    v[j] = tab[t1 < a.adam_tab_len ? t1 : a.adam_tab_len - 1];
+  }
+}
+template <int J>
+DTP_DEV void adam_tab_store(float2* __restrict__ lds, int n, int tid, const float2 (&v)[J]) {
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    if (tid + j * kBlock < n) lds[tid + j * kBlock] = v[j];
+}
+
 template <class S>
 struct TrainSmem {
   float wb[Scal<S>::LW];  // backward + forward weight blocks (mlp_scalar.h)
@@ -143,6 +162,11 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   // the step number: from the host when it knows it (the persistent engine), so the
   // first dataset indices can be requested without waiting for the counter's load
   const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
+  // the host's Adam-scalar table (persistent engine): the first kAdamTab entries are
+  // loaded with the prologue's other global reads (one memory round trip for all)
+  const bool htab = kAdam && a.adam_tab && a.host_t0 >= 0;
+  float2 tabv[kAdamTab / kBlock];
+  if (htab) adam_tab_load<kAdamTab / kBlock>(a, t0, 0, tid, tabv);
   // 32-bit step bookkeeping, advanced incrementally (no 64-bit divisions per step)
   const bool explicit_idx = !FAST && smp.mode == SAMPLER_EXPLICIT;
   int epoch = explicit_idx ? 0 : t0 / smp.steps_per_epoch;
@@ -252,6 +276,12 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   // table entry e holds the scalars of step number t0 + base + e + 1
   auto fill_adam = [&](int base) {
     const int n = min(kAdamTab, a.n_steps - base);  // short launches (eager / graph) fill only what they use
+    if (htab) {
+      float2 v[kAdamTab / kBlock];
+      if (base) adam_tab_load<kAdamTab / kBlock>(a, t0, base, tid, v);
+      adam_tab_store<kAdamTab / kBlock>(sm.adam_tab, n, tid, base ? v : tabv);
+      return;
+    }
     for (int e = tid; e < n; e += kBlock) {
       const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
       const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
@@ -549,6 +579,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
     vr[k] = own ? a.opt_v[(size_t)model * P + p] : 0.f;
   }
   const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
+  const bool htab = a.adam_tab && a.host_t0 >= 0;
+  float2 tabv[kAdamTab / kBlock];
+  if (htab) adam_tab_load<kAdamTab / kBlock>(a, t0, 0, tid, tabv);
   int epoch = t0 / smp.steps_per_epoch;
   int bi = t0 - epoch * smp.steps_per_epoch;
   auto fast_index = [&](int ep_, int b_) -> int {
@@ -615,6 +648,12 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
   bool nvalid = fast_gather(fidx0, nx, ny);
   auto fill_adam = [&](int base) {
     const int n = min(kAdamTab, a.n_steps - base);
+    if (htab) {
+      float2 v[kAdamTab / kBlock];
+      if (base) adam_tab_load<kAdamTab / kBlock>(a, t0, base, tid, v);
+      adam_tab_store<kAdamTab / kBlock>(sm.adam_tab, n, tid, base ? v : tabv);
+      return;
+    }
     for (int e = tid; e < n; e += kBlock) {
       const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
       const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);

@@ -112,6 +112,15 @@ class FusedTrainer:
                 raise NotImplementedError(f"no fused train kernel for {spec}")
             # scalar-weight workspace of the fused step (csrc/mlp_scalar.h), scratch
             self.wsp = torch.zeros(n_models * ws, dtype=torch.float32, device=dev)
+            # Adam's per-step scalars, formed once on the host (f64, the kernels' own
+            # arithmetic): a persistent launch loads them with its other prologue reads
+            self._adam_tab = None
+            if self.optim.name == "adam":
+                from ..ops.optim import adam_bias_table
+
+                tab = adam_bias_table(self.optim)
+                if tab is not None:
+                    self._adam_tab = torch.from_numpy(tab).to(dev)
             if geom.mode == SAMPLER_DIST_SHUFFLE:
                 if self.cfg.sampler not in ("torch", "device"):
                     raise ValueError(f"sampler {self.cfg.sampler!r}: torch or device")
@@ -266,7 +275,7 @@ class FusedTrainer:
             smp.mode = nat.SAMPLER_EXPLICIT
             smp.batch = batch_override or g.batch
         xg = self._xgmi
-        return nat.TrainArgs(
+        a = nat.TrainArgs(
             nat.ptr(self.X), nat.ptr(self.Y), nat.ptr(idx), nat.ptr(self.params), nat.ptr(self.m), nat.ptr(self.v),
             nat.ptr(self.step_ctr), nat.ptr(self.comm_buf), nat.ptr(self.loss_log),
             nat.ptr(xg.status) if xg else None, nat.ptr(xg.peer_table) if xg else None,
@@ -277,6 +286,10 @@ class FusedTrainer:
             # xGMI modes sum the W gradients in-kernel -> DDP averaging 1/W there;
             # MODE_GRAD writes local means (the flat optimizer applies 1/W)
             self._hyper(1.0 / self.world if mode in (nat.MODE_XGMI_ADAM, nat.MODE_XGMI_SGD) else 1.0))
+        tab = getattr(self, "_adam_tab", None)
+        if tab is not None:
+            a.adam_tab, a.adam_tab_len = nat.ptr(tab), tab.shape[0]
+        return a
 
     def _update_mode(self) -> int:
         if self.comm == "xgmi":
@@ -525,6 +538,11 @@ class FusedTrainer:
                 "optim": self.optim.__dict__}
 
     def load_state_dict(self, sd: dict):
+        # the persistent launch takes its step number (sampler cursor AND Adam bias
+        # corrections) from the host mirror t, so the device counters must equal it
+        steps = torch.as_tensor(sd["step"]).reshape(-1).tolist()
+        if any(int(s) != int(sd["t"]) for s in steps):
+            raise ValueError(f"inconsistent engine state: step counters {steps} but t = {sd['t']}")
         self.params.copy_(sd["params"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])

@@ -57,6 +57,45 @@ def adam_update_ref(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.
     p.addcdiv_(m, denom, value=-(cfg.lr / bc1))
 
 
+def adam_bias_table(cfg: "OptimConfig", max_len: int = 1 << 22):
+    """Adam's per-step scalars as the fused kernels use them: row t = {lr / (1 - b1^t),
+    sqrt(1 - b2^t)} in float32, formed in float64 exactly as the kernels' own fill does
+    (``pow_int``: repeated squaring, ``csrc/dtp_common.h``), so a launch reading this
+    table is bitwise the launch that forms the scalars itself.  The table ends at the
+    first t where both corrections are exactly 1.0 in float64; every later step uses
+    that last row.  None if that takes more than ``max_len`` steps (beta ~ 1)."""
+    import numpy as np
+
+    b1, b2 = float(cfg.betas[0]), float(cfg.betas[1])
+
+    def pow_int(b: float, t: "np.ndarray") -> "np.ndarray":
+        r = np.ones(t.shape, dtype=np.float64)
+        base = np.full(t.shape, b, dtype=np.float64)
+        e = t.copy()
+        while e.any():
+            r = np.where(e & 1, r * base, r)
+            base = base * base
+            e >>= 1
+        return r
+
+    n = 1024
+    while True:
+        t = np.arange(n, dtype=np.int64)
+        bc1 = 1.0 - pow_int(b1, t)
+        bc2 = 1.0 - pow_int(b2, t)
+        done = np.nonzero((bc1 == 1.0) & (bc2 == 1.0))[0]
+        if done.size or n >= max_len:
+            break
+        n *= 2
+    if not done.size:
+        return None
+    T = int(done[0])
+    with np.errstate(divide="ignore"):
+        tab = np.stack([(float(cfg.lr) / bc1[:T + 1]).astype(np.float32),
+                        np.sqrt(bc2[:T + 1]).astype(np.float32)], axis=1)
+    return tab
+
+
 def sgd_update_ref(p: torch.Tensor, buf: torch.Tensor, g: torch.Tensor, first: bool, cfg: OptimConfig) -> None:
     if cfg.weight_decay:
         g = g + cfg.weight_decay * p

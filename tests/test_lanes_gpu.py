@@ -132,3 +132,31 @@ def test_lanes_agree_with_one_lane_kernel(tmp_path):
     for flag in ("2", "4"):
         torch.testing.assert_close(outs[flag]["l"], outs["1"]["l"], rtol=1e-4, atol=1e-6)
         torch.testing.assert_close(outs[flag]["p"], outs["1"]["p"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("batch", [256, 64])
+def test_host_adam_table_bitwise_equals_kernel_fill(batch):
+    """The persistent launch reads Adam's per-step scalars from the host-built table
+    (ops/optim.py:adam_bias_table) with its prologue loads; without the table the kernel
+    forms them itself in f64.  Same bits, across a table refill (1100 steps > 1024) and
+    past the table's saturated end (t0 near 37k)."""
+    X, Y = ToyData(n=512, seed=12).device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=6)
+    init = _init(TOY_SPEC, 77)
+    res = []
+    for host in (True, False):
+        tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), EngineConfig(steps_per_launch=1100),
+                          init_params=init)
+        assert (tr._adam_tab is not None) and tr._adam_tab.shape[0] > 30000
+        if not host:
+            tr._adam_tab = None
+        tr.train(1100)
+        # jump the step counter near / past the table's end (37413 rows for the default betas)
+        tr.t = 37400
+        tr.step_ctr.fill_(37400)
+        tr.train(40)
+        tr.synchronize()
+        res.append((tr.params.clone(), tr.losses(0, 1100), tr.losses(37400, 37440)))
+        tr.close()
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
