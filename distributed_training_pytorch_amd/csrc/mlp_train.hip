@@ -990,9 +990,12 @@ int pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
     return e ? atoi(e) : 0;
   }();
   if (!fast || a.bf16 || a.smp.n * (in + out) > dtp::kLaneData) return 1;
-  int want = a.smp.batch <= dtp::kBlock / 4 ? 4 : (a.smp.batch <= dtp::kBlock / 2 ? 2 : 1);
+  // the largest batch a step sees: a rank's share of the epoch can be smaller than the
+  // configured batch (strong scaling: 512 samples over 8 ranks -> 64 of batch 256)
+  const int b = min(a.smp.batch, a.smp.num_samples);
+  int want = b <= dtp::kBlock / 4 ? 4 : (b <= dtp::kBlock / 2 ? 2 : 1);
   if (forced == 1 || forced == 2 || forced == 4) want = forced;
-  return a.smp.batch <= dtp::kBlock / want ? want : 1;
+  return b <= dtp::kBlock / want ? want : 1;
 }
 
 TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode, int* lanes = nullptr) {
@@ -1065,7 +1068,7 @@ int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
 
 template <class S, int L>
 int launch_lanes_profile(const DtpTrainArgs* a, hipStream_t st) {
-  if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM) || a->smp.batch > dtp::kBlock / L ||
+  if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM) || min(a->smp.batch, a->smp.num_samples) > dtp::kBlock / L ||
       a->smp.n * (S::IN + S::OUT) > dtp::kLaneData)
     return set_err(-2, "the lanes profile instance needs the FAST configuration and batch <= 256 / L");
   hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, true>), dim3(a->n_models), dim3(dtp::kBlock),

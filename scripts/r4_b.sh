@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 4, session b: strong-scaling lanes pick, trainer spec check, split stream diagnosis, bench lines
+export TMPDIR=/tmp
+D=${1:-r4b}
+mkdir -p gpurun_out/$D
+bash scripts/gpu_steps.sh \
+  "300|$D/tests|python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_trainer_fused_gpu.py tests/test_bench_gpu.py" \
+  "200|$D/diag_streams|for m in per_device cumask torch prio; do python scripts/diag_split_streams.py \$m; done" \
+  "200|$D/rocprof_cumask|timeout -k 10 150 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$D/prof_cumask -o cumask -- python3 scripts/diag_split_streams.py cumask" \
+  "200|$D/bench_k20|for i in 1 2 3 4 5; do python bench.py --steps 20 --warmup 5; done" \
+  "100|$D/bench_default|python bench.py" \
+  "400|$D/share|for w in 2 4 8; do timeout 120 python -m torch.distributed.run --nnodes=1 --nproc-per-node \$w --master-addr 127.0.0.1 --master-port 2961\$w bench.py --gpus \$w --share-gpu --steps 2000 --warmup 100 || exit 3; done"
