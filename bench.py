@@ -132,7 +132,7 @@ def main():
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
                     else "Feistel shuffle", "cu_mask": a.cu_mask,
                     # lanes per sample of the fused step (1, or 2 / 4: csrc/mlp_lanes.h for batches <= 128 / 64)
-                    "lanes_per_sample": runner.lanes}
+                    "lanes_per_sample": runner.lanes, "waves_per_cu": runner.kernel_waves}
 
     # the timed region is bracketed by an all-rank barrier + synchronize on both sides;
     # ranks of the in-kernel xGMI engine use the framework's device barrier (one xGMI

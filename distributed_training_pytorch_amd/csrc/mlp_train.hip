@@ -11,6 +11,7 @@
 //                       demo_one_model_multi_gpu.py:17-42 equivalent).
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "dtp_api.h"
@@ -38,20 +39,20 @@ constexpr int kWaves = kBlock / kWave;
 // entries base + tid + j * kBlock (j < J) of the host's Adam table for a launch starting
 // at step t0: {lr / (1 - b1^t1), sqrt(1 - b2^t1)} with t1 = t0 + e + 1, clamped to the
 // table's saturated last row
-template <int J>
+template <int J, int NTH = kBlock>
 DTP_DEV void adam_tab_load(const DtpTrainArgs& a, int t0, int base, int tid, float2 (&v)[J]) {
   const float2* __restrict__ tab = reinterpret_cast<const float2*>(a.adam_tab);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const long long t1 = (long long)t0 + base + tid + j * kBlock + 1;
+    const long long t1 = (long long)t0 + base + tid + j * NTH + 1;
     v[j] = tab[t1 < a.adam_tab_len ? t1 : a.adam_tab_len - 1];
   }
 }
-template <int J>
+template <int J, int NTH = kBlock>
 DTP_DEV void adam_tab_store(float2* __restrict__ lds, int n, int tid, const float2 (&v)[J]) {
 #pragma unroll
   for (int j = 0; j < J; ++j)
-    if (tid + j * kBlock < n) lds[tid + j * kBlock] = v[j];
+    if (tid + j * NTH < n) lds[tid + j * NTH] = v[j];
 }
 
 template <class S>
@@ -537,25 +538,41 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
 // floats of dataset staged in LDS by the lanes kernel (strong scaling: n = 512 x 3)
 constexpr int kLaneData = 4096;
 
-template <class S, int L>
+// staging areas of one wave: the packed first/last tile (or the last layer's and the first
+// layer's when they do not pack) and ONE area shared by the hidden layers -- a wave's LDS
+// operations execute in order, so layer l-1's staging writes land after layer l's MFMA
+// operand reads were issued (the constant-1 bias column, written once, is the same
+// column in every hidden tile)
+template <class S>
+DTP_HD constexpr int lane_areas() { return Scal<S>::PACK ? 2 : 3; }
+template <class S>
+DTP_HD constexpr int lane_area(int l) {
+  return (Scal<S>::PACK && (l == 0 || l == S::NL - 1)) ? 0 : (l == S::NL - 1 ? 0 : (l == 0 ? 2 : 1));
+}
+
+template <class S, int L, int NW>
 struct LaneSmem {
   using C = LaneCfg<S, L>;
   alignas(16) float wb[C::pad4(C::LW)];
-  alignas(16) float stg[kWaves][Scal<S>::NT][2 * C::AREA];  // per wave, per tile: dz area, h area
-  alignas(16) float red[kWaves][Scal<S>::NT * 256];         // per-wave partial dW tiles
+  alignas(16) float stg[NW][lane_areas<S>()][2 * C::AREA];  // per wave, per area: dz operand, h operand
+  alignas(16) float red[NW][Scal<S>::NT * 256];             // per-wave partial dW tiles
   alignas(16) float2 adam_tab[kAdamTab];
   alignas(16) float data[kLaneData];
   float sink[4];
 };
 
-template <class S, int L, int MODE, bool PROF = false>
-__global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(DtpTrainArgs a) {
+// NW waves per workgroup (4: one per SIMD; 8: two per SIMD, for batches of 256 / L < B <= 512 / L)
+template <class S, int L, int MODE, bool PROF = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
+void mlp_train_lanes_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
   using C = LaneCfg<S, L>;
-  constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT, NO = C::NO, TS = C::TS, H = S::H;
+  constexpr int NTH = 64 * NW;                 // threads of the workgroup
+  constexpr int NPT = (S::P + NTH - 1) / NTH;  // parameters owned per thread (optimizer, exchange)
+  constexpr int NL = S::NL, P = S::P, NT = SC::NT, NO = C::NO, TS = C::TS, H = S::H;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM;
   static_assert(MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM, "the lanes step serves the Adam modes");
-  __shared__ __align__(16) LaneSmem<S, L> sm;
+  __shared__ __align__(16) LaneSmem<S, L, NW> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
   const int part = lane & (L - 1);          // this lane's slice of every hidden layer
@@ -580,8 +597,8 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
   }
   const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
   const bool htab = a.adam_tab && a.host_t0 >= 0;
-  float2 tabv[kAdamTab / kBlock];
-  if (htab) adam_tab_load<kAdamTab / kBlock>(a, t0, 0, tid, tabv);
+  float2 tabv[kAdamTab / NTH];
+  if (htab) adam_tab_load<kAdamTab / NTH, NTH>(a, t0, 0, tid, tabv);
   int epoch = t0 / smp.steps_per_epoch;
   int bi = t0 - epoch * smp.steps_per_epoch;
   auto fast_index = [&](int ep_, int b_) -> int {
@@ -604,19 +621,19 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
   int fidx = fast_index(e2, b2);
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
   unsigned long long xwait = 0;
-  for (int e = tid; e < C::pad4(C::LW); e += kBlock) sm.wb[e] = 0.f;
-  for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
-  for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * S::IN + e] = a.Y[e];
+  for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
+  for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
+  for (int e = tid; e < smp.n * S::OUT; e += NTH) sm.data[smp.n * S::IN + e] = a.Y[e];
   const int yoff = smp.n * S::IN;
   // this wave's staging areas: zero (unwritten rows / columns stay finite), then the
   // constant-1 bias columns of every tile, written once per launch
   {
     float* s0 = &sm.stg[wave][0][0];
-    for (int e = lane; e < NT * 2 * C::AREA; e += kWave) s0[e] = 0.f;
+    for (int e = lane; e < lane_areas<S>() * 2 * C::AREA; e += kWave) s0[e] = 0.f;
     static_for<0, NL>([&](auto LC) {
       constexpr int l = decltype(LC)::value;
       constexpr int col = SC::coloff(l) + S::din(l);
-      float* hb = &sm.stg[wave][SC::tile(l)][C::AREA];
+      float* hb = &sm.stg[wave][lane_area<S>(l)][C::AREA];
       for (int e = lane; e < 4 * TS; e += kWave) hb[(e / TS) * C::QS + col * TS + e % TS] = 1.f;
     });
   }
@@ -649,12 +666,12 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
   auto fill_adam = [&](int base) {
     const int n = min(kAdamTab, a.n_steps - base);
     if (htab) {
-      float2 v[kAdamTab / kBlock];
-      if (base) adam_tab_load<kAdamTab / kBlock>(a, t0, base, tid, v);
-      adam_tab_store<kAdamTab / kBlock>(sm.adam_tab, n, tid, base ? v : tabv);
+      float2 v[kAdamTab / NTH];
+      if (base) adam_tab_load<kAdamTab / NTH, NTH>(a, t0, base, tid, v);
+      adam_tab_store<kAdamTab / NTH, NTH>(sm.adam_tab, n, tid, base ? v : tabv);
       return;
     }
-    for (int e = tid; e < n; e += kBlock) {
+    for (int e = tid; e < n; e += NTH) {
       const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
       const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
       sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
@@ -710,7 +727,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
     float dzp[C::NOP];  // this lane's slice of the current layer's output gradient
     {  // last layer: stage (dz, loss, own slice of its input), input-gradient slice
       constexpr int l = NL - 1;
-      float* tl = &sm.stg[wave][SC::tile(l)][0];
+      float* tl = &sm.stg[wave][lane_area<S>(l)][0];
       if (part == 0) {
         static_for<0, S::OUT>([&](auto JC) {
           tl[wslot + (SC::rowoff(l) + decltype(JC)::value) * TS] = dzl[decltype(JC)::value];
@@ -747,7 +764,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
     // hidden layers NL-2 .. 1: block B of layer l in registers, block l-1 prefetched
     auto hidden = [&](auto LC, const auto& B, auto& nb) {
       constexpr int l = decltype(LC)::value;
-      float* tl = &sm.stg[wave][SC::tile(l)][0];
+      float* tl = &sm.stg[wave][lane_area<S>(l)][0];
+      // the previous layer's MFMA operand reads of this area were issued before these writes
+      __builtin_amdgcn_sched_barrier(0);
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
         if (slot_ok(k)) {
@@ -805,7 +824,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
     };
     hidden_rest(hidden_rest, std::integral_constant<int, NL - 2>{}, bt2);
     {  // layer 0: its dW tile only (packed with the last layer's when they fit)
-      float* tl = &sm.stg[wave][SC::tile(0)][0];
+      float* tl = &sm.stg[wave][lane_area<S>(0)][0];
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
         if (slot_ok(k)) tl[wpart + (SC::rowoff(0) + k) * TS] = dzp[k];
@@ -839,18 +858,18 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
     for (int k = 0; k < NPT; ++k) {
       float s = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) s += sm.red[ww][tp[k]];
+      for (int ww = 0; ww < NW; ++ww) s += sm.red[ww][tp[k]];
       g[k] = s;
     }
     float lsum = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) lsum += sm.red[ww][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+    for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
     const float mean_loss = lsum * inv;
     DTP_STAMP(5);
     float gloss = mean_loss;
     if constexpr (kXgmi) {
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, &xwait);
+      gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, &xwait);
     }
     const int lslot_now = lslot;
     roll(epoch, bi);
@@ -871,7 +890,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_lanes_kernel(
         *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
       }
     }
-    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, kBlock) : 0) && a.loss_log) {
+    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, NTH) : 0) && a.loss_log) {
       const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
       a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
     }
@@ -959,7 +978,8 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   // n >= world: the FAST gather wraps a padded-list position with ONE subtraction of n
   // (positions stay below n + world - 1), where the generic sampler takes q % n
   const bool ring = s.perm && s.perm_epochs > 0 && (s.perm_epochs & (s.perm_epochs - 1)) == 0;
-  return a.cache_data && a.loss == DTP_LOSS_MSE && s.batch <= dtp::kBlock && s.mode == dtp::SAMPLER_TABLE && ring &&
+  return a.cache_data && a.loss == DTP_LOSS_MSE && min(s.batch, s.num_samples) <= dtp::kBlock &&
+         s.mode == dtp::SAMPLER_TABLE && ring &&
          s.n >= s.world && s.n * (in + ydim) <= dtp::kDataCache &&
          a.hp.slope >= 0.f && a.hp.slope <= 1.f;
 }
@@ -969,47 +989,70 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   X(2, 10, 5, 1)                 \
   X(2, 10, 5, 4)
 
-template <class S, int L, int MODE>
+template <class S, int L, int MODE, int NW>
 void launch_lanes(const DtpTrainArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, MODE>), dim3(a.n_models), dim3(dtp::kBlock), 0, st, a);
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, MODE, false, NW>), dim3(a.n_models), dim3(64 * NW), 0, st,
+                     a);
 }
 
-template <class S, int L>
+template <class S, int L, int NW>
 TrainLaunchFn lanes_fn(int mode) {
-  if (mode == DTP_MODE_ADAM) return &launch_lanes<S, L, DTP_MODE_ADAM>;
-  if (mode == DTP_MODE_XGMI_ADAM) return &launch_lanes<S, L, DTP_MODE_XGMI_ADAM>;
+  if (mode == DTP_MODE_ADAM) return &launch_lanes<S, L, DTP_MODE_ADAM, NW>;
+  if (mode == DTP_MODE_XGMI_ADAM) return &launch_lanes<S, L, DTP_MODE_XGMI_ADAM, NW>;
   return nullptr;
 }
 
-// lanes per sample of the step instance for this launch: 4 for per-rank batches <= 64,
-// 2 for <= 128, else 1 (the one-lane kernel).  DTP_LANES=1|2|4 forces a choice (A/B
-// runs; a forced L whose batch bound does not hold falls back to 1).
-int pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
-  static const int forced = [] {
+// the step instance of a launch: lanes per sample and waves per workgroup
+struct LanePick {
+  int L = 1, NW = 4;
+};
+
+// 4 lanes per sample for per-rank batches <= 64, 2 for <= 128, else the one-lane kernel
+// (L = 1).  DTP_LANES=<L>[x<NW>] forces a choice (A/B runs; NW = 8 runs two waves per
+// SIMD, 512 / L samples); a forced pick whose batch bound does not hold falls back to 1.
+LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
+  static const LanePick forced = [] {
+    LanePick f{0, 4};
     const char* e = getenv("DTP_LANES");
-    return e ? atoi(e) : 0;
+    if (e) {
+      f.L = atoi(e);
+      const char* x = strchr(e, 'x');
+      if (x) f.NW = atoi(x + 1);
+    }
+    return f;
   }();
-  if (!fast || a.bf16 || a.smp.n * (in + out) > dtp::kLaneData) return 1;
+  LanePick r;
+  if (!fast || a.bf16 || a.smp.n * (in + out) > dtp::kLaneData) return r;
   // the largest batch a step sees: a rank's share of the epoch can be smaller than the
   // configured batch (strong scaling: 512 samples over 8 ranks -> 64 of batch 256)
   const int b = min(a.smp.batch, a.smp.num_samples);
-  int want = b <= dtp::kBlock / 4 ? 4 : (b <= dtp::kBlock / 2 ? 2 : 1);
-  if (forced == 1 || forced == 2 || forced == 4) want = forced;
-  return b <= dtp::kBlock / want ? want : 1;
+  r.L = b <= dtp::kBlock / 4 ? 4 : (b <= dtp::kBlock / 2 ? 2 : 1);
+  if ((forced.L == 1 || forced.L == 2 || forced.L == 4) && (forced.NW == 4 || forced.NW == 8)) {
+    r.L = forced.L;
+    r.NW = forced.L == 1 ? 4 : forced.NW;
+  }
+  if (b > 64 * r.NW / r.L) r = LanePick{};
+  return r;
 }
 
-TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode, int* lanes = nullptr) {
+TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode,
+                            LanePick* pick = nullptr) {
   const bool fast = fast_path_ok(a, in, out, mode);
-  const int L = pick_lanes(a, in, out, fast);
-  if (lanes) *lanes = L;
-  if (L > 1) {
+  const LanePick lp = pick_lanes(a, in, out, fast);
+  if (pick) *pick = lp;
+  if (lp.L > 1 && lp.NW == 4) {
 #define X(I, H, N, O)                                                                                   \
   if (in == I && h == H && nl == N && out == O)                                                         \
-    return L == 4 ? lanes_fn<dtp::Stage<I, H, N, O, false>, 4>(mode) : lanes_fn<dtp::Stage<I, H, N, O, false>, 2>(mode);
+    return lp.L == 4 ? lanes_fn<dtp::Stage<I, H, N, O, false>, 4, 4>(mode)                              \
+                     : lanes_fn<dtp::Stage<I, H, N, O, false>, 2, 4>(mode);
     DTP_TRAIN_SHAPES(X)
 #undef X
-    if (lanes) *lanes = 1;
   }
+  if (lp.L > 1 && lp.NW == 8 && in == 2 && h == 10 && nl == 5 && out == 1) {  // two waves per SIMD: toy shape
+    using T = dtp::Stage<2, 10, 5, 1, false>;
+    return lp.L == 4 ? lanes_fn<T, 4, 8>(mode) : lanes_fn<T, 2, 8>(mode);
+  }
+  if (pick) *pick = LanePick{};
   if (a.bf16) {
 #define X(I, H, N, O) \
   if (in == I && h == H && nl == N && out == O) return train_fn<dtp::Stage<I, H, N, O, false, true>>(mode, fast);
@@ -1054,7 +1097,7 @@ struct TrainEngine {
   DtpTrainArgs a;
   TrainLaunchFn fn;
   int mode;
-  int lanes;  // lanes per sample of the chosen instance (1: mlp_train_kernel)
+  LanePick pick;  // lanes per sample / waves of the chosen instance (L = 1: mlp_train_kernel)
 };
 
 template <class S>
@@ -1066,12 +1109,12 @@ int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
   return check_launch("mlp_train_kernel<prof>");
 }
 
-template <class S, int L>
+template <class S, int L, int NW = 4>
 int launch_lanes_profile(const DtpTrainArgs* a, hipStream_t st) {
-  if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM) || min(a->smp.batch, a->smp.num_samples) > dtp::kBlock / L ||
+  if (!fast_path_ok(*a, S::IN, S::OUT, DTP_MODE_ADAM) || min(a->smp.batch, a->smp.num_samples) > 64 * NW / L ||
       a->smp.n * (S::IN + S::OUT) > dtp::kLaneData)
-    return set_err(-2, "the lanes profile instance needs the FAST configuration and batch <= 256 / L");
-  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, true>), dim3(a->n_models), dim3(dtp::kBlock),
+    return set_err(-2, "the lanes profile instance needs the FAST configuration and batch <= 64 NW / L");
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, true, NW>), dim3(a->n_models), dim3(64 * NW),
                      0, st, *a);
   return check_launch("mlp_train_lanes_kernel<prof>");
 }
@@ -1100,7 +1143,9 @@ int dtp_mlp_workspace_floats(int in, int h, int nl, int out) {
 // bytes of one rank's receive buffer of the fused step's xGMI exchange
 // ([parity 2][model][src rank][slot] of 16-byte granules, xgmi_core.h)
 long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world) {
-  const int npt = (P + dtp::kBlock - 1) / dtp::kBlock;
+  // sized for the instance with the most granules: 512 threads (8-wave lanes step), one
+  // parameter per thread
+  const int npt = (P + 2 * dtp::kBlock - 1) / (2 * dtp::kBlock);
   return 2ll * n_models * world * dtp::xgmi_slot16(P, npt) * 16ll;
 }
 
@@ -1124,8 +1169,8 @@ int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mod
 
 void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
   if (validate_train(a, mode)) return nullptr;
-  int lanes = 1;
-  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode, &lanes);
+  LanePick lp;
+  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode, &lp);
   if (!fn) {
     set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
     return nullptr;
@@ -1134,21 +1179,22 @@ void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int 
   e->a = *a;
   e->fn = fn;
   e->mode = mode;
-  e->lanes = lanes;
+  e->pick = lp;
   return e;
 }
 
 // lanes per sample of the engine's kernel instance (1 = one lane per sample)
 int dtp_train_engine_lanes(void* h) {
   auto* e = static_cast<TrainEngine*>(h);
-  return e ? e->lanes : set_err(-1, "null engine");
+  return e ? e->pick.L : set_err(-1, "null engine");
 }
 
-// lanes per sample the step would use for these arguments (0: no fused instance)
+// lanes per sample (low byte) and waves per workgroup (<< 8) the step would use for
+// these arguments (0: no fused instance)
 int dtp_mlp_train_lanes(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
   if (validate_train(a, mode)) return 0;
-  int lanes = 1;
-  return resolve_train(*a, in, h, nl, out, mode, &lanes) ? lanes : 0;
+  LanePick lp;
+  return resolve_train(*a, in, h, nl, out, mode, &lp) ? (lp.L | (lp.NW << 8)) : 0;
 }
 
 // n_steps iterations in ONE persistent launch on `stream`, starting at step t0 (the
@@ -1173,9 +1219,13 @@ int dtp_mlp_train_profile(const DtpTrainArgs* a, void* stream) {
 
 // same for the lanes step (toy shape), L = 2 or 4
 int dtp_mlp_train_profile_lanes(const DtpTrainArgs* a, int lanes, void* stream) {
-  if (lanes == 2) return launch_lanes_profile<dtp::Stage<2, 10, 5, 1, false>, 2>(a, (hipStream_t)stream);
-  if (lanes == 4) return launch_lanes_profile<dtp::Stage<2, 10, 5, 1, false>, 4>(a, (hipStream_t)stream);
-  return set_err(-1, "lanes must be 2 or 4");
+  using T = dtp::Stage<2, 10, 5, 1, false>;
+  const int L = lanes & 0xff, NW = lanes >> 8 ? lanes >> 8 : 4;
+  if (L == 2 && NW == 4) return launch_lanes_profile<T, 2>(a, (hipStream_t)stream);
+  if (L == 4 && NW == 4) return launch_lanes_profile<T, 4>(a, (hipStream_t)stream);
+  if (L == 2 && NW == 8) return launch_lanes_profile<T, 2, 8>(a, (hipStream_t)stream);
+  if (L == 4 && NW == 8) return launch_lanes_profile<T, 4, 8>(a, (hipStream_t)stream);
+  return set_err(-1, "lanes must be 2 or 4 (| waves << 8, waves 4 or 8)");
 }
 
 int dtp_sampler_indices(const dtp::SamplerCfg* s, long long t0, int n_steps, int* out, void* stream) {

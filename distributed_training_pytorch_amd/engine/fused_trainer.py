@@ -134,6 +134,15 @@ class FusedTrainer:
         one-lane kernel, 2 / 4 = the several-lanes step (``csrc/mlp_lanes.h``) that the
         native dispatch picks for per-rank batches <= 128 / <= 64 (0: no fused kernel,
         e.g. a CPU engine or the RCCL path's grad kernel)."""
+        return self._pick() & 0xFF
+
+    @property
+    def kernel_waves(self) -> int:
+        """Waves per workgroup of the fused step instance (4: one per SIMD; 8: two, the
+        several-lanes step over 512 / L samples); 0 without a fused kernel."""
+        return self._pick() >> 8
+
+    def _pick(self) -> int:
         if not self.native or self.comm in ("rccl", "host"):
             return 0
         a = self._train_args(1, self._update_mode(), None)

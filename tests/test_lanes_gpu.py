@@ -160,3 +160,44 @@ def test_host_adam_table_bitwise_equals_kernel_fill(batch):
         tr.close()
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
+
+
+_W8_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.toy_data import ToyData
+from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
+from distributed_training_pytorch_amd.ops.optim import OptimConfig
+dev = torch.device("cuda", 0)
+X, Y = ToyData(n=512, seed=31).device_tensors(dev)
+g = torch.Generator().manual_seed(3)
+init = [(torch.randn(TOY_SPEC.P, generator=g) * 0.4).to(dev) for _ in range(2)]
+tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch={batch}, seed=2), OptimConfig(lr=1e-2),
+                  EngineConfig(steps_per_launch=6), init_params=init)
+pick = (tr.lanes, tr.kernel_waves)
+tr.train({steps})
+tr.synchronize()
+torch.save({{"p": tr.params.cpu(), "l": tr.losses(0, {steps}), "pick": pick, "init": [p.cpu() for p in init]}},
+           {out!r})
+"""
+
+
+@pytest.mark.parametrize("force,batch", [("2x8", 256), ("2x8", 200), ("4x8", 128)])
+def test_two_waves_per_simd_instances_match_torch(force, batch, tmp_path):
+    """The 8-wave lanes step (two waves per SIMD, 512 / L samples per step; DTP_LANES=<L>x8)
+    against autograd + torch.optim.Adam, including a short last batch (200)."""
+    steps = 11
+    out = str(tmp_path / "w8.pt")
+    env = dict(os.environ, DTP_LANES=force)
+    r = subprocess.run([sys.executable, "-c", _W8_SCRIPT.format(root=ROOT, batch=batch, steps=steps, out=out)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = torch.load(out, weights_only=True)
+    assert res["pick"] == (int(force[0]), 8)
+    X, Y = ToyData(n=512, seed=31).device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=2)
+    ref_p, ref_l = torch_train(TOY_SPEC, res["init"], X, Y, [EpochIndexStream(geom)], steps, OptimConfig(lr=1e-2))
+    torch.testing.assert_close(res["l"], ref_l, rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(res["p"], ref_p, rtol=1e-3, atol=2e-5)
