@@ -686,6 +686,18 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   const int rdoff = (lane >> 4) * C::QS + (lane & 15) * TS;
   // is slot k of this lane's slice a real unit (k*L + part < H)?
   auto slot_ok = [&](int k) { return C::EXACT || part * NO + k < H; };
+  // A staging write of a lane with nothing to stage (a padding slot, a part other than 0
+  // for the per-sample rows) goes to row / column 15 of its sample slot when no tile uses
+  // it -- D[15][*] and D[*][15] are never read -- so the writes are branch-free
+  constexpr bool kSink = H <= 14 && SC::lossrow() <= 14 && (!SC::PACK || S::IN + 1 + H <= 14);
+  auto put = [&](float* tl, int area, int off, bool ok, float v) {
+    if constexpr (kSink) {
+      tl[area + (ok ? off : wslot + 15 * TS)] = v;
+    } else {
+      if (ok) tl[area + off] = v;
+    }
+  };
+  const bool p0 = part == 0;
   __syncthreads();
 
   for (int it = 0; it < a.n_steps; ++it) {
@@ -728,15 +740,13 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     {  // last layer: stage (dz, loss, own slice of its input), input-gradient slice
       constexpr int l = NL - 1;
       float* tl = &sm.stg[wave][lane_area<S>(l)][0];
-      if (part == 0) {
-        static_for<0, S::OUT>([&](auto JC) {
-          tl[wslot + (SC::rowoff(l) + decltype(JC)::value) * TS] = dzl[decltype(JC)::value];
-        });
-        tl[wslot + SC::lossrow() * TS] = lpart;
-      }
+      static_for<0, S::OUT>([&](auto JC) {
+        put(tl, 0, wslot + (SC::rowoff(l) + decltype(JC)::value) * TS, p0, dzl[decltype(JC)::value]);
+      });
+      put(tl, 0, wslot + SC::lossrow() * TS, p0, lpart);
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
-        if (slot_ok(k)) tl[C::AREA + wpart + (SC::coloff(l) + k) * TS] = st.own[l - 1][k];
+        put(tl, C::AREA, wpart + (SC::coloff(l) + k) * TS, slot_ok(k), st.own[l - 1][k]);
       });
       f32x2 g[C::NPR];
       static_for<0, C::NPR>([&](auto RC) { g[decltype(RC)::value] = f32x2{0.f, 0.f}; });
@@ -769,10 +779,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
-        if (slot_ok(k)) {
-          tl[wpart + (SC::rowoff(l) + k) * TS] = dzp[k];
-          tl[C::AREA + wpart + (SC::coloff(l) + k) * TS] = st.own[l - 1][k];
-        }
+        put(tl, 0, wpart + (SC::rowoff(l) + k) * TS, slot_ok(k), dzp[k]);
+        put(tl, C::AREA, wpart + (SC::coloff(l) + k) * TS, slot_ok(k), st.own[l - 1][k]);
       });
       __builtin_amdgcn_wave_barrier();
       const auto to = lane_tile_ops<C>(tl, rdoff);
@@ -827,13 +835,11 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       float* tl = &sm.stg[wave][lane_area<S>(0)][0];
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
-        if (slot_ok(k)) tl[wpart + (SC::rowoff(0) + k) * TS] = dzp[k];
+        put(tl, 0, wpart + (SC::rowoff(0) + k) * TS, slot_ok(k), dzp[k]);
       });
-      if (part == 0) {
-        static_for<0, S::IN>([&](auto IC) {
-          tl[C::AREA + wslot + (SC::coloff(0) + decltype(IC)::value) * TS] = x0[decltype(IC)::value];
-        });
-      }
+      static_for<0, S::IN>([&](auto IC) {
+        put(tl, C::AREA, wslot + (SC::coloff(0) + decltype(IC)::value) * TS, p0, x0[decltype(IC)::value]);
+      });
       __builtin_amdgcn_wave_barrier();
       const auto to = lane_tile_ops<C>(tl, rdoff);
       f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
