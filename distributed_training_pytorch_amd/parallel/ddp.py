@@ -31,7 +31,10 @@ from . import comm_util
 
 
 class FlatDDP(nn.Module):
-    def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 64.0, first_bucket_mb: float = 1.0,
+    # bucket_cap_mb / first_bucket_mb: torch DDP's defaults (25 MB, 1 MiB first bucket,
+    # torch/nn/parallel/distributed.py).  The round-3 default of 64 MB had no measurement
+    # behind it; scripts/ab_bucket_cap.sh A/Bs the cap on the wide MLP.
+    def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
                  flat_params: torch.Tensor | None = None, flat_grad: torch.Tensor | None = None,
                  broadcast: bool = True, comm: str = "auto"):
         super().__init__()
