@@ -133,7 +133,7 @@ class SplitStageArgs(ctypes.Structure):
         ("dp_world", c_int),
         ("dp_rank", c_int),
         ("optim", c_int),
-        ("pad_", c_int),
+        ("link_local", c_int),
         ("smp", SamplerCfg),
         ("hp", Hyper),
     ]

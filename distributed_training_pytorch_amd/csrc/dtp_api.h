@@ -117,7 +117,8 @@ struct DtpSplitStageArgs {
   int dp_world;
   int dp_rank;
   int optim;              // DTP_MODE_ADAM or DTP_MODE_SGD
-  int pad_;
+  int link_local;         // bit 0: the previous stage, bit 1: the next stage is on this GPU
+                          // (device-scope link: plain device memory, sc1); else system scope
   dtp::SamplerCfg smp;
   DtpHyper hp;            // grad_scale = 1 / dp_world
 };

@@ -32,9 +32,14 @@ namespace dtp {
 
 constexpr int kSplitCache = 8192;  // floats of dataset staged in LDS (first / last stage)
 
+// cache policy of a link: sc1 = device scope (both stages on one GPU: the granules meet in
+// the device's last-level cache, no round trip to HBM), sc0 | sc1 = system scope
+// (neighbour on another GPU, uncached fine-grained buffer written over xGMI)
+constexpr int kDevCoherent = 16;
+
 // one lane's message: N floats as ceil(N/2) granules at granule index slot * G
 template <int N>
-DTP_DEV void link_send(void* buf, int slot, unsigned ep, const float (&v)[16], bool valid) {
+DTP_DEV void link_send(void* buf, int slot, unsigned ep, const float (&v)[16], bool valid, bool local) {
   constexpr int G = (N + 1) / 2;
   if (!valid) return;
   const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(buf);
@@ -42,14 +47,15 @@ DTP_DEV void link_send(void* buf, int slot, unsigned ep, const float (&v)[16], b
   for (int g = 0; g < G; ++g) {
     const uint32_t x0 = __float_as_uint(v[2 * g]), x1 = 2 * g + 1 < N ? __float_as_uint(v[2 * g + 1]) : 0u;
     const u32x4 q = {ep, x0, x1, xgmi_check(ep, x0, x1)};
-    __builtin_amdgcn_raw_buffer_store_b128(q, rs, (slot * G + g) * 16, 0, kSysCoherent);
+    if (local) __builtin_amdgcn_raw_buffer_store_b128(q, rs, (slot * G + g) * 16, 0, kDevCoherent);
+    else __builtin_amdgcn_raw_buffer_store_b128(q, rs, (slot * G + g) * 16, 0, kSysCoherent);
   }
 }
 
 // poll this lane's granules of epoch ep in the local receive buffer (bounded)
 template <int N>
 DTP_DEV void link_recv(const void* buf, int slot, unsigned ep, float (&v)[16], bool valid, int* status,
-                       int timeout_us, bool& dead) {
+                       int timeout_us, bool& dead, bool local) {
   constexpr int G = (N + 1) / 2;
   static_assert(G <= 16, "message too wide");
   const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(buf);
@@ -64,7 +70,9 @@ DTP_DEV void link_recv(const void* buf, int slot, unsigned ep, float (&v)[16], b
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       x[g] = u32x4{0u, 0u, 0u, 0u};
-      if ((pend >> g) & 1u) x[g] = __builtin_amdgcn_raw_buffer_load_b128(ms, (slot * G + g) * 16, 0, kSysCoherent);
+      if ((pend >> g) & 1u)
+        x[g] = local ? __builtin_amdgcn_raw_buffer_load_b128(ms, (slot * G + g) * 16, 0, kDevCoherent)
+                     : __builtin_amdgcn_raw_buffer_load_b128(ms, (slot * G + g) * 16, 0, kSysCoherent);
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -180,6 +188,7 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
   __syncthreads();
 
   bool link_dead = __hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const bool prev_local = a.link_local & 1, next_local = (a.link_local >> 1) & 1;
   const XgmiCtx dp{a.dp_peers, a.status + 2, a.dp_world, a.dp_rank, 1, a.timeout_us};
   const bool use_dp = a.dp_world > 1;
   float* red = &sm.stage[0][0];
@@ -204,7 +213,7 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
         h[0][i] = valid ? (cached ? sm.data[di * S::IN + i] : a.X[(size_t)di * S::IN + i]) : 0.f;
       });
     } else {
-      link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead);
+      link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead, prev_local);
     }
     mlp_forward<S>(sm.w, h, slope);
 
@@ -214,9 +223,9 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
     for (int j = 0; j < 16; ++j) dz[j] = 0.f;
     const float inv = 1.f / (float)(bsz * S::OUT);
     if constexpr (!LAST) {
-      link_send<S::OUT>(a.act_out, tid, ep, h[NL], valid);
+      link_send<S::OUT>(a.act_out, tid, ep, h[NL], valid, next_local);
       float go[16];
-      link_recv<S::OUT>(a.grad_in, tid, ep, go, valid, a.status, a.timeout_us, link_dead);
+      link_recv<S::OUT>(a.grad_in, tid, ep, go, valid, a.status, a.timeout_us, link_dead, next_local);
       static_for<0, S::OUT>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
         const float d = S::FINAL_ACT ? go[j] * leaky_grad_from_out(h[NL][j], slope) : go[j];
@@ -240,7 +249,7 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
     for (int l = 0; l < NL; ++l) acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
     float dx[16];
     mlp_backward<S, !FIRST, LAST>(sm.w, h, dz, &sm.stage[wave][0], acc, slope, lane, dx);
-    if constexpr (!FIRST) link_send<S::IN>(a.grad_out, tid, ep, dx, valid);
+    if constexpr (!FIRST) link_send<S::IN>(a.grad_out, tid, ep, dx, valid, prev_local);
 
     // ---- reduce the per-wave tiles (staging area reused once every wave is done)
     __syncthreads();

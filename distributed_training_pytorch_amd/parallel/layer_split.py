@@ -366,14 +366,31 @@ class FusedLayerSplit:
         self.loss_log = torch.zeros(log_cap, device=self.devices[-1])
         self.X = X.to(self.devices[0]).contiguous().float()
         self.Y = Y.to(self.devices[-1]).contiguous().float()
-        # link buffers: act into stage s+1 (on its device), grad into stage s (on its device)
+        # link buffers: act into stage s+1 (on its device), grad into stage s (on its device).
+        # Neighbours on one GPU talk through plain device memory at device scope (the
+        # granules meet in the last-level cache); across GPUs through uncached fine-grained
+        # buffers at system scope (xGMI).  DTP_SPLIT_LOCAL_LINKS=0 forces the latter (A/B).
+        import os
+
+        local_ok = os.environ.get("DTP_SPLIT_LOCAL_LINKS", "1") != "0"
         self._owned: list[tuple[int, int]] = []  # (device index, pointer)
+        self._link_tensors: list[torch.Tensor] = []
         self.act_buf, self.grad_buf = [None] * K, [None] * K
+        self.link_local = [local_ok and self.devices[s] == self.devices[s + 1] for s in range(K - 1)]
         for s in range(K - 1):
             width = self.stage_specs[s].out_features
             nbytes = int(lib.dtp_split_link_bytes(width, geom.batch))
-            self.act_buf[s + 1] = self._alloc(self.devices[s + 1], nbytes)
-            self.grad_buf[s] = self._alloc(self.devices[s], nbytes)
+            if self.link_local[s]:
+                for buf in ("act", "grad"):
+                    t = torch.zeros(nbytes, dtype=torch.uint8, device=self.devices[s])
+                    self._link_tensors.append(t)
+                    if buf == "act":
+                        self.act_buf[s + 1] = t.data_ptr()
+                    else:
+                        self.grad_buf[s] = t.data_ptr()
+            else:
+                self.act_buf[s + 1] = self._alloc(self.devices[s + 1], nbytes)
+                self.grad_buf[s] = self._alloc(self.devices[s], nbytes)
         # per-stage data-parallel exchange (the stage's gradient over the ranks)
         self._dp = [None] * K
         if self.world > 1:
@@ -441,6 +458,8 @@ class FusedLayerSplit:
                 a.cache_data = 1
                 a.dp_world, a.dp_rank = self.world, self.rank
                 a.optim = nat.MODE_ADAM if self.optim.name == "adam" else nat.MODE_SGD
+                a.link_local = (int(s > 0 and self.link_local[s - 1])
+                                | (int(s + 1 < K and self.link_local[s]) << 1))
                 a.smp = geom.to_native()
                 if dev in self.rings and (s == 0 or s == K - 1):
                     self.rings[dev].native(a.smp)
@@ -573,3 +592,4 @@ class FusedLayerSplit:
             with torch.cuda.device(dev_index):
                 self.lib.dtp_free(ctypes.c_void_p(ptr))
         self._owned = []
+        self._link_tensors = []
