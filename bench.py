@@ -78,6 +78,30 @@ def parse():
     return ap.parse_args()
 
 
+def pin_host_thread(dev) -> int | None:
+    """Pin this (launching, synchronizing) thread to one CPU of the GPU's NUMA node: the
+    K-step call is a launch, a wait and a synchronize, so a migration or a remote-node
+    wakeup lands inside the timed region.  The CPU comes from the GPU's PCI
+    ``local_cpulist`` within this process's allowed set (each local rank takes its own);
+    None when the box does not expose it."""
+    if dev.type != "cuda" or not hasattr(os, "sched_setaffinity"):
+        return None
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        spec = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
+        local = set()
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            local.update(range(int(lo), int(hi or lo) + 1))
+        allowed = sorted(local & os.sched_getaffinity(0)) or sorted(os.sched_getaffinity(0))
+        cpu = allowed[int(os.environ.get("LOCAL_RANK", "0")) % len(allowed)]
+        os.sched_setaffinity(0, {cpu})
+        return cpu
+    except (OSError, ValueError, AttributeError, IndexError):
+        return None
+
+
 def main():
     a = parse()
     if torch.cuda.device_count() > 0:  # counting devices does not initialise the GPU
@@ -99,6 +123,7 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
     dev = bootstrap.bind_device(env)
+    pinned = pin_host_thread(dev) if os.environ.get("DTP_BENCH_PIN", "1") != "0" else None
     if world > 1 or a.impl == "stock":  # the stock loop wraps its models in torch DDP even at W=1
         bootstrap.init_process_group(env, "gloo" if (a.share_gpu or dev.type == "cpu") else "nccl", dev)
     n = 512 * world if a.scaling == "weak" else 512
@@ -129,6 +154,7 @@ def main():
         # the xGMI timeout word is checked right after the timed region (check_comm below)
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm,
+                    "host_cpu": pinned,
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
                     else "Feistel shuffle", "cu_mask": a.cu_mask,
                     # lanes per sample of the fused step (1, or 2 / 4: csrc/mlp_lanes.h for batches <= 128 / 64)
