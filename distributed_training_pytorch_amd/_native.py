@@ -259,6 +259,8 @@ def _declare(lib):
         "dtp_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
         "dtp_stream_sync": (c_int, [c_void_p]),
         "dtp_stream_create_cu_mask": (c_int, [ctypes.POINTER(ctypes.c_uint), c_int, ctypes.POINTER(c_void_p)]),
+        "dtp_stream_create_priority": (c_int, [c_int, P(c_void_p)]),
+        "dtp_stream_priority_range": (c_int, [P(c_int), P(c_int)]),
         "dtp_stream_destroy": (c_int, [c_void_p]),
         "dtp_device_sync_check": (c_int, []),
         "dtp_graph_capture_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
@@ -412,6 +414,25 @@ def set_wait_mode(mode: str | None = None) -> str:
 def native_enabled() -> bool:
     """DTP_NATIVE=0 forces the PyTorch reference path (debug only; never on a timed run)."""
     return os.environ.get("DTP_NATIVE", "1") != "0"
+
+
+def priority_stream(device, priority: int) -> "torch.cuda.ExternalStream":
+    """A torch stream at a HIP stream priority (``hipStreamCreateWithPriority``, lower =
+    higher priority); it lives for the rest of the process."""
+    lib = require(torch.device(device))
+    out = ctypes.c_void_p()
+    with torch.cuda.device(torch.device(device)):
+        check(lib.dtp_stream_create_priority(int(priority), ctypes.byref(out)), "dtp_stream_create_priority")
+    return torch.cuda.ExternalStream(out.value, device=torch.device(device))
+
+
+def stream_priority_levels(device) -> list[int]:
+    """The device's stream priority levels, highest priority first."""
+    lib = require(torch.device(device))
+    least, greatest = ctypes.c_int(), ctypes.c_int()
+    with torch.cuda.device(torch.device(device)):
+        check(lib.dtp_stream_priority_range(ctypes.byref(least), ctypes.byref(greatest)), "dtp_stream_priority_range")
+    return list(range(greatest.value, least.value + 1))
 
 
 def cu_masked_stream(device, cus) -> "torch.cuda.ExternalStream":

@@ -160,6 +160,25 @@ int dtp_stream_create_cu_mask(const unsigned* mask, int words, void** out) {
   return 0;
 }
 
+// A stream of the given priority (hipStreamCreateWithPriority; lower = higher priority).
+// The layer-split engine's stages that share a GPU (persistent kernels that wait on each
+// other) launch on streams of distinct priority levels: a hardware queue has one priority,
+// so two such streams never sit in one in-order queue.  (Measured: CU-masked streams got
+// separate queues yet ran one kernel after the other -- the second dispatch started when
+// the first ended; profiles/r4_split_streams/.)
+int dtp_stream_create_priority(int priority, void** out) {
+  *out = nullptr;
+  hipStream_t s = nullptr;
+  RT_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  *out = s;
+  return 0;
+}
+
+int dtp_stream_priority_range(int* least, int* greatest) {
+  RT_CHECK(hipDeviceGetStreamPriorityRange(least, greatest));
+  return 0;
+}
+
 int dtp_stream_destroy(void* stream) {
   if (stream) RT_CHECK(hipStreamDestroy((hipStream_t)stream));
   return 0;

@@ -52,9 +52,24 @@ class ToyModel(nn.Module):
             self._flat = flat
         return self._flat
 
+    def _packed(self) -> bool:
+        """Are the parameters still consecutive views of ``_flat``?  Another owner (e.g.
+        ``FlatDDP``) may have re-packed them into its own flat buffer."""
+        ps = list(self.layers.parameters())
+        base, es, o = self._flat.data_ptr(), self._flat.element_size(), 0
+        for p in ps:
+            if p.data_ptr() != base + o * es or not p.is_contiguous():
+                return False
+            o += p.numel()
+        return o == self._flat.numel()
+
     @property
     def flat_params(self) -> torch.Tensor:
-        return self._flat
+        """The parameters as one flat vector: the packed buffer itself, or -- once another
+        owner re-packed the parameters -- a fresh concatenation of their current values."""
+        if self._packed():
+            return self._flat
+        return torch.cat([p.detach().reshape(-1) for p in self.layers.parameters()])
 
     def _apply(self, fn, recurse=True):
         out = super()._apply(fn, recurse)
@@ -63,7 +78,13 @@ class ToyModel(nn.Module):
 
     def load_flat_(self, flat: torch.Tensor) -> None:
         with torch.no_grad():
-            self._flat.copy_(flat.reshape(-1).to(self._flat))
+            if self._packed():
+                self._flat.copy_(flat.reshape(-1).to(self._flat))
+                return
+            o, flat = 0, flat.reshape(-1)
+            for p in self.layers.parameters():  # re-packed elsewhere: write the live storage
+                p.copy_(flat[o:o + p.numel()].view_as(p).to(p))
+                o += p.numel()
 
     def uses_fused_kernel(self) -> bool:
         if self._fused is None:

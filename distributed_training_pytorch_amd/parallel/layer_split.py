@@ -411,10 +411,11 @@ class FusedLayerSplit:
         # launch = "per_device": the stages that share a GPU run as ONE launch (one
         # workgroup each: co-resident by construction), one stream per GPU.
         # launch = "per_stage": every stage is its own launch on its own stream -- what a
-        # node with one GPU per stage runs anyway; stages that share a GPU then get
-        # streams with DISJOINT CU masks, i.e. separate hardware queues (two persistent
-        # kernels that wait on each other must never sit behind one another in one
-        # in-order queue), which rehearses the multi-GPU launch path on one GPU
+        # node with one GPU per stage runs anyway.  Stages that share a GPU then get
+        # streams of DISTINCT priority levels, so no two of those persistent kernels (which
+        # wait on each other) sit in one in-order hardware queue; this rehearses the
+        # multi-GPU launch path on one GPU.  (CU-masked streams were tried first: they got
+        # separate queues but dispatched one after the other, profiles/r4_split_streams/.)
         if launch not in ("per_device", "per_stage"):
             raise ValueError(f"launch={launch!r}: per_device or per_stage")
         self.launch_mode = launch
@@ -427,10 +428,13 @@ class FusedLayerSplit:
         self.streams = {}
         for k, v in self.groups.items():
             dev = self.key_dev[k]
-            shared = sum(1 for d in self.devices if d == dev) > 1
-            if launch == "per_stage" and shared:
-                j = [s for s in range(K) if self.devices[s] == dev].index(v[0])
-                self.streams[k] = nat.cu_masked_stream(dev, [2 * j, 2 * j + 1])
+            on_dev = [s for s in range(K) if self.devices[s] == dev]
+            if launch == "per_stage" and len(on_dev) > 1:
+                levels = nat.stream_priority_levels(dev)
+                if len(on_dev) > len(levels):
+                    raise ValueError(f"launch='per_stage' with {len(on_dev)} stages on {dev}: only {len(levels)} "
+                                     "stream priority levels; use launch='per_device'")
+                self.streams[k] = nat.priority_stream(dev, levels[on_dev.index(v[0])])
             else:
                 self.streams[k] = torch.cuda.Stream(device=dev)
         self.t = 0

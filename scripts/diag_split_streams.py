@@ -25,7 +25,9 @@ def main():
     init = torch.randn(TOY_SPEC.P, generator=torch.Generator().manual_seed(0)) * 0.4
     eng = FusedLayerSplit(TOY_SPEC, [dev, dev], ds.X, ds.Y, geom, OptimConfig(lr=1e-3), init,
                           launch="per_device" if mode == "per_device" else "per_stage", timeout_us=200_000)
-    if mode == "torch":
+    if mode == "cumask":
+        eng.streams = {k: nat.cu_masked_stream(dev, [2 * k, 2 * k + 1]) for k in eng.streams}
+    elif mode == "torch":
         eng.streams = {k: torch.cuda.Stream(device=dev) for k in eng.streams}
     elif mode == "prio":
         eng.streams = {k: torch.cuda.Stream(device=dev, priority=-1 if k else 0) for k in eng.streams}

@@ -151,3 +151,22 @@ def test_loss_and_optimizer_options_gloo_dp(loss, ocfg):
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[0][0], rp, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(res[0][1], rl, rtol=1e-5, atol=1e-6)
+
+
+def test_toy_flat_params_follow_a_repack():
+    """FlatDDP re-packs a module's parameters into its own flat buffer; ToyModel's
+    flat_params / load_flat_ must then read and write the live parameters, not the
+    abandoned packing."""
+    from distributed_training_pytorch_amd.models.toy import ToyModel
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(0)
+    m = ToyModel()
+    FlatDDP(m)  # one process: no broadcast; re-packs the parameters
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(1.0)
+    live = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert torch.equal(m.flat_params, live)
+    m.load_flat_(torch.zeros_like(live))
+    assert all(bool((p == 0).all()) for p in m.parameters())
