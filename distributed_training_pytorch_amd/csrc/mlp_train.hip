@@ -528,7 +528,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     }
     if (tid == 0) a.step[model] = t0 + a.n_steps;
     if (kXgmi && tid == 0) a.epoch[model] = xepoch;
-    if (kXgmi && tid == 0 && model == 0) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps);
+    if (kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
     stamp_launch(21);
   }
 }
@@ -920,7 +920,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   }
   if (tid == 0) a.step[model] = t0 + a.n_steps;
   if (kXgmi && tid == 0) a.epoch[model] = xepoch;
-  if (kXgmi && tid == 0 && model == 0) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps);
+  if (kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
 }
 
 // ------------------------------------------------------------------------------

@@ -251,13 +251,21 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
   return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid, waited);
 }
 
-// the fused step's exchange diagnostics in the status block: [4..6) u64 wait ticks and
-// [6..8) u64 exchanges of thread 0 of model 0, accumulated over launches (the host
-// zeroes them around a timed region)
-DTP_DEV void xgmi_record_wait(int* status, unsigned long long ticks, unsigned long long n) {
-  if (!status) return;
-  atomicAdd(reinterpret_cast<unsigned long long*>(status + 4), ticks);
-  atomicAdd(reinterpret_cast<unsigned long long*>(status + 6), n);
+// the fused step's exchange diagnostics in the status block, for model 0's workgroup:
+// [4..6) u64 += the launch's exchange-wait ticks of its SLOWEST thread (the step cannot
+// pass its closing barrier before that thread has every peer granule), [6..8) u64 +=
+// the launch's exchanges; [8..10) is the per-launch max scratch.  Accumulated over
+// launches; the host zeroes them around a timed region.  Called by EVERY thread of the
+// workgroup at the end of the launch (contains a barrier).
+DTP_DEV void xgmi_record_wait(int* status, unsigned long long ticks, unsigned long long n, int tid) {
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(status + 4);
+  atomicMax(w + 2, ticks);
+  __syncthreads();  // every thread's max has landed (device-coherent atomics, then the barrier)
+  if (tid == 0) {
+    const unsigned long long m = atomicExch(w + 2, 0ull);
+    atomicAdd(w, m);
+    atomicAdd(w + 1, n);
+  }
 }
 
 }  // namespace dtp

@@ -492,14 +492,15 @@ class FusedTrainer:
         return buf[:n * P].view(n, P), buf[n * P:n * P + n]
 
     def exchange_stats_reset(self) -> None:
-        """Zero the in-kernel exchange's wait counters (status words [4..8), stream-ordered)."""
+        """Zero the in-kernel exchange's wait counters (status words [4..10), stream-ordered)."""
         if self._xgmi is not None:
-            self._xgmi.status[4:8].zero_()
+            self._xgmi.status[4:10].zero_()
 
     def exchange_stats(self) -> tuple[float, int] | None:
-        """(microseconds thread 0 of model 0 spent between publishing its gradient granules
-        and accepting the last peer granule, summed over the exchanges since the last
-        reset; number of exchanges) -- None without the in-kernel xGMI exchange.  Syncs."""
+        """(microseconds model 0's slowest thread spent between publishing its gradient
+        granules and accepting its last peer granule, summed over the launches since the
+        last reset; number of exchanges) -- None without the in-kernel xGMI exchange.
+        Syncs."""
         if self._xgmi is None:
             return None
         w = self._xgmi.status[4:8].cpu().view(torch.int64).tolist()
