@@ -311,10 +311,12 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
 }
 
 // (IN, H, NL, OUT, FINAL_ACT, FIRST): the contiguous layer ranges of the toy model
-// as pipeline stages (first stages read the 2-feature input; stages that end inside
+// as pipeline stages (the first entry: the whole model as ONE stage -- the split code's
+// baseline with no links, scripts/split_cost.py) (first stages read the 2-feature input; stages that end inside
 // the network carry the LeakyReLU of their last layer and are not last); the shape
 // id of a stage is its position in this list
 #define DTP_SPLIT_SHAPES(X)   \
+  X(2, 10, 5, 1, false, 1)    \
   X(2, 10, 1, 10, true, 1)    \
   X(2, 10, 2, 10, true, 1)    \
   X(2, 10, 3, 10, true, 1)    \
