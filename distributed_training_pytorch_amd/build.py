@@ -40,7 +40,8 @@ COMMON_FLAGS = [
 # -ffp-contract=off where the optimizer math lives: every fused multiply-add there is
 # an explicit fmaf, so kernel instances scheduled differently round identically
 SOURCE_FLAGS = {"mlp_train.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-ffp-contract=off"],
-                "optim.hip": ["-ffp-contract=off"], "split_train.hip": ["-ffp-contract=off"]}
+                "optim.hip": ["-ffp-contract=off"],
+                "split_train.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-ffp-contract=off"]}
 
 
 def hipcc() -> str:

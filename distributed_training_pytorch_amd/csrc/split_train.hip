@@ -25,6 +25,7 @@
 // neighbour can never hang the GPU.
 #include "dtp_api.h"
 #include "mlp_core.h"
+#include "mlp_pipe.h"
 #include "optim_core.h"
 #include "xgmi_core.h"
 
@@ -107,7 +108,21 @@ struct SplitSmem {
   float2 adam_tab[kSplitAdamTab];  // {lr / (1 - b1^t), sqrt(1 - b2^t)} of steps t0 + base + e + 1
 };
 
-constexpr int kSplitSmemBytes = 80 * 1024;  // the largest stage's SplitSmem
+// stages of >= 2 layers: the fused step's software-pipelined schedule (mlp_pipe.h)
+// with its LDS blocks (mlp_scalar.h), plus layer 0 row-major for the input gradient
+// a non-first stage sends back; one staging area per wave (two when the first and last
+// layer tiles pack), reused for the cross-wave reduction
+template <class S>
+struct SplitPipeSmem {
+  static constexpr int AREAS = Scal<S>::PACK ? 2 : 1;
+  float wb[Scal<S>::LW];
+  float w0r[S::dout(0) * S::pad4(S::IN)];
+  float stage[kBlock / kWave][AREAS][2 * kStgArr];
+  float data[kSplitCache];
+  float2 adam_tab[kSplitAdamTab];
+};
+
+constexpr int kSplitSmemBytes = 120 * 1024;  // the largest stage's SplitSmem / SplitPipeSmem
 
 // One pipeline stage, n_steps iterations.  FIRST: gathers the batch inputs from the
 // dataset; LAST: gathers the targets and computes the MSE loss; otherwise the
@@ -115,7 +130,7 @@ constexpr int kSplitSmemBytes = 80 * 1024;  // the largest stage's SplitSmem
 // split_multi_kernel (all the stages that share a GPU are one launch, so they are
 // co-resident by construction: no reliance on separate hardware queues).
 template <class S, bool FIRST, bool LAST>
-DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
+DTP_DEV void split_stage_body_v1(const DtpSplitStageArgs& a, unsigned char* smem) {
   constexpr int NL = S::NL, P = S::P, NPT = S::NPT;
   static_assert(kBlock / kWave * NL * 256 <= kBlock / kWave * 2 * kStgArr, "reduction tiles fit the staging area");
   static_assert(sizeof(SplitSmem<S>) <= kSplitSmemBytes, "stage LDS exceeds the shared block");
@@ -310,6 +325,249 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
   if (tid == 0) a.step[0] = t0 + a.n_steps;
 }
 
+// One pipeline stage of >= 2 layers on the fused step's pipelined schedule: the next
+// layer's weight block streams in during the current layer, the dW MFMA K-steps ride
+// between the input-gradient rows (mlp_pipe.h).  Same protocol, sampler, exchange and
+// optimizer as split_stage_body_v1 (the one-layer stages keep that one).
+template <class S, bool FIRST, bool LAST>
+DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* smem) {
+  using SC = Scal<S>;
+  constexpr int NL = S::NL, P = S::P, NPT = S::NPT, NT = SC::NT;
+  static_assert(NL >= 2, "one-layer stages run split_stage_body_v1");
+  static_assert(NT * 256 <= 2 * kStgArr, "a wave's reduction tiles fit its staging area");
+  static_assert(sizeof(SplitPipeSmem<S>) <= kSplitSmemBytes, "stage LDS exceeds the shared block");
+  SplitPipeSmem<S>& sm = *reinterpret_cast<SplitPipeSmem<S>*>(smem);
+  const bool adam = a.optim == DTP_MODE_ADAM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const SamplerCfg smp = a.smp;
+  const float slope = a.hp.slope;
+  constexpr int XW = FIRST ? S::IN : 0;
+  constexpr int YW = LAST ? S::OUT : 0;
+  constexpr int IP0 = S::pad4(S::IN);
+
+  // ---- prologue: owned parameters + moments in registers, weight blocks and dataset in LDS
+  float pw[NPT], mr[NPT], vr[NPT];
+  int pfl[NPT], pb[NPT], tp[NPT], p0r[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = NPT * tid + k;
+    const bool own = p < P;
+    pw[k] = own ? a.params[p] : 0.f;
+    mr[k] = own ? a.opt_m[p] : 0.f;
+    vr[k] = (own && adam) ? a.opt_v[p] : 0.f;
+    int pf_;
+    scal_pos<S>(own ? p : 0, pf_, pb[k], tp[k], pfl[k]);
+    if (!own) pfl[k] = pb[k] = -1;
+    // layer-0 weights, row-major: the input gradient of a non-first stage
+    const int q = p - S::gw(0);
+    p0r[k] = (!FIRST && own && q >= 0 && q < S::gb(0)) ? (q / S::IN) * IP0 + q % S::IN : -1;
+  }
+  for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
+  for (int e = tid; e < S::dout(0) * IP0; e += kBlock) sm.w0r[e] = 0.f;
+  const bool cached = a.cache_data && smp.n * (XW + YW) <= kSplitCache;
+  if (cached) {
+    if constexpr (FIRST)
+      for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
+    if constexpr (LAST)
+      for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * XW + e] = a.Y[e];
+  }
+  const int t0 = a.step[0];
+  int epoch = t0 / smp.steps_per_epoch;
+  int bi = t0 - epoch * smp.steps_per_epoch;
+  auto index_at = [&](int ep, int b) -> int {
+    if constexpr (!(FIRST || LAST)) {
+      return 0;
+    } else {
+      BatchPos bp;
+      bp.epoch = ep;
+      bp.start = b * smp.batch;
+      bp.size = min(smp.batch, smp.num_samples - bp.start);
+      uint32_t keys[4];
+      epoch_keys(smp, ep, keys);
+      return tid < bp.size ? sample_index(smp, bp, keys, tid) : 0;
+    }
+  };
+  int di_next = index_at(epoch, bi);
+  auto fill_adam = [&](int base) {
+    const int n = min(kSplitAdamTab, a.n_steps - base);
+    for (int e = tid; e < n; e += kBlock) {
+      const uint64_t t1 = (uint64_t)t0 + (uint64_t)base + (uint64_t)e + 1u;
+      const double bc1 = 1.0 - pow_int(a.hp.beta1, t1), bc2 = 1.0 - pow_int(a.hp.beta2, t1);
+      sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
+    }
+  };
+  if (adam) fill_adam(0);
+  auto scatter = [&]() {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if (pfl[k] >= 0) sm.wb[pfl[k]] = pw[k];
+      if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
+      if (p0r[k] >= 0) sm.w0r[p0r[k]] = pw[k];
+    }
+  };
+  __syncthreads();  // pads zeroed before the owners scatter
+  scatter();
+  __syncthreads();
+
+  bool link_dead = __hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const bool prev_local = a.link_local & 1, next_local = (a.link_local >> 1) & 1;
+  const XgmiCtx dp{a.dp_peers, a.status + 2, a.dp_world, a.dp_rank, 1, a.timeout_us};
+  const bool use_dp = a.dp_world > 1;
+  float* const stg_pack = &sm.stage[wave][0][0];
+  float* const stg_hid = &sm.stage[wave][SplitPipeSmem<S>::AREAS - 1][0];
+
+  for (int it = 0; it < a.n_steps; ++it) {
+    const int t = t0 + it;
+    const unsigned ep = (unsigned)t + 1u;
+    const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
+    const bool valid = tid < bsz;
+    const int di = di_next;
+    if (++bi == smp.steps_per_epoch) {
+      bi = 0;
+      ++epoch;
+    }
+    if (it + 1 < a.n_steps) di_next = index_at(epoch, bi);
+    const float inv = 1.f / (float)(bsz * S::OUT);
+    // ---- forward (the first block is read here; the others stream in layer by layer)
+    float h[NL + 1][16];
+    if constexpr (FIRST) {
+      static_for<0, S::IN>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        h[0][i] = valid ? (cached ? sm.data[di * S::IN + i] : a.X[(size_t)di * S::IN + i]) : 0.f;
+      });
+    } else {
+      link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead, prev_local);
+    }
+    BBlk<S, NL - 1> pbt;
+    TopB2<S> pbt2;
+    {
+      FBlk<S, 0> pb0;
+      pb0.template load<0, FBlk<S, 0>::NR>(sm.wb);
+      pipe_forward<S, 0>(sm.wb, pb0, h, slope, pbt, pbt2);
+    }
+    // ---- output gradient: from the next stage, or the MSE loss (last stage)
+    float dz[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dz[j] = 0.f;
+    float lpart = 0.f;
+    if constexpr (!LAST) {
+      link_send<S::OUT>(a.act_out, tid, ep, h[NL], valid, next_local);
+      float go[16];
+      link_recv<S::OUT>(a.grad_in, tid, ep, go, valid, a.status, a.timeout_us, link_dead, next_local);
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float d = S::FINAL_ACT ? go[j] * leaky_grad_from_out(h[NL][j], slope) : go[j];
+        dz[j] = valid ? d : 0.f;
+      });
+    } else {
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float y = valid ? (cached ? sm.data[smp.n * XW + di * S::OUT + j] : a.Y[(size_t)di * S::OUT + j]) : 0.f;
+        const float d = h[NL][j] - y;
+        lpart = valid ? fmaf(d, d, lpart) : lpart;
+        dz[j] = valid ? 2.f * d * inv : 0.f;
+      });
+    }
+    // ---- backward: input-gradient chain (VALU) + dW tiles (MFMA, K = samples)
+    f32x4 acc[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const PipeBwdCtx<S> pc{sm.wb, stg_pack, stg_hid, lane, slope, lpart};
+    if constexpr (NL >= 3) {
+      pipe_backward<S>(pc, pbt, pbt2, h, dz, acc);
+    } else {  // two layers: the top layer, then layer 0's tile
+      NoBlk none;
+      pipe_bwd_layer<S, 1>(pc, pbt, h, dz, acc, none);
+      float* stg = pipe_stage<S, 0>(pc, h, dz);
+      __builtin_amdgcn_wave_barrier();
+      acc[SC::tile(0)] = TileKind<S>::outer(stg, stg + kStgArr, acc[SC::tile(0)], lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (!FIRST) {  // dz now holds layer 0's output gradient: dx = W_0^T dz
+      float dx[16];
+      static_for<0, S::IN>([&](auto IC) { dx[decltype(IC)::value] = 0.f; });
+      static_for<0, S::dout(0)>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        static_for<0, S::IN>([&](auto IC) {
+          constexpr int i = decltype(IC)::value;
+          dx[i] = fmaf(sm.w0r[j * IP0 + i], dz[j], dx[i]);
+        });
+      });
+      link_send<S::IN>(a.grad_out, tid, ep, dx, valid, prev_local);
+    }
+    // ---- each wave parks its partial tiles in its own staging area (its staging reads
+    // were issued before these writes); one barrier publishes them
+    {
+      const int q = lane >> 4, col = lane & 15;
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stg_pack[tt * 256 + (4 * q + r) * 16 + col] = acc[tt][r];
+    }
+    __syncthreads();
+    float g[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kBlock / kWave; ++ww) v += sm.stage[ww][0][tp[k]];
+      g[k] = v;
+    }
+    float loss = 0.f;
+    if constexpr (LAST) {
+      float ls = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kBlock / kWave; ++ww)
+        ls += sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+      loss = ls * inv;
+    }
+    float gloss = loss;
+    if (use_dp) gloss = xgmi_allreduce_slots<NPT>(dp, 0, P, g, loss, ep, tid);
+    // ---- optimizer (registers) + weight refresh (LDS)
+    const float gs = a.hp.grad_scale;
+    if (adam) {
+      AdamScalars as = adam_consts(a.hp);
+      const float2 sc = sm.adam_tab[it % kSplitAdamTab];
+      as.step_size = sc.x;
+      as.bc2_sqrt = sc.y;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        if (pfl[k] >= 0) adam_update(pw[k], mr[k], vr[k], g[k] * gs, as);
+    } else {
+      const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        if (pfl[k] >= 0) sgd_update(pw[k], mr[k], g[k] * gs, lr, mom, wd, t == 0);
+    }
+    scatter();
+    if constexpr (LAST) {
+      const int owner = use_dp ? xgmi_loss_tid<NPT>(P, kBlock) : 0;
+      if (tid == owner && a.loss_log) a.loss_log[t % a.loss_log_cap] = use_dp ? gloss * gs : loss;
+    }
+    __syncthreads();  // new weights visible; reduction tiles consumed before the next staging writes
+    if (adam && (it + 1) % kSplitAdamTab == 0 && it + 1 < a.n_steps) {
+      fill_adam(it + 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int p = NPT * tid + k;
+    if (p < P) {
+      a.params[p] = pw[k];
+      a.opt_m[p] = mr[k];
+      if (adam) a.opt_v[p] = vr[k];
+    }
+  }
+  if (tid == 0) a.step[0] = t0 + a.n_steps;
+}
+
+template <class S, bool FIRST, bool LAST>
+DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
+  if constexpr (S::NL >= 2) split_stage_body_pipe<S, FIRST, LAST>(a, smem);
+  else split_stage_body_v1<S, FIRST, LAST>(a, smem);
+}
+
 // (IN, H, NL, OUT, FINAL_ACT, FIRST): the contiguous layer ranges of the toy model
 // as pipeline stages (the first entry: the whole model as ONE stage -- the split code's
 // baseline with no links, scripts/split_cost.py) (first stages read the 2-feature input; stages that end inside
@@ -330,7 +588,7 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
   X(10, 10, 4, 1, false, 0)
 
 // every stage placed on one GPU, one workgroup each (blockIdx.x = local stage)
-__global__ __launch_bounds__(kBlock) void split_multi_kernel(DtpSplitLaunch) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void split_multi_kernel(DtpSplitLaunch) {
   __shared__ __align__(16) unsigned char smem[kSplitSmemBytes];
   const int b = blockIdx.x;
   // this workgroup's stage arguments straight from the kernarg segment (uniform
