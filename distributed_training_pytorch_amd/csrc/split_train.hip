@@ -562,9 +562,13 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
   if (tid == 0) a.step[0] = t0 + a.n_steps;
 }
 
+#ifndef DTP_SPLIT_PIPE
+#define DTP_SPLIT_PIPE 1  // 0: every stage on the round-3 body (A/B builds, build.variant)
+#endif
+
 template <class S, bool FIRST, bool LAST>
 DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
-  if constexpr (S::NL >= 2) split_stage_body_pipe<S, FIRST, LAST>(a, smem);
+  if constexpr (DTP_SPLIT_PIPE && S::NL >= 2) split_stage_body_pipe<S, FIRST, LAST>(a, smem);
   else split_stage_body_v1<S, FIRST, LAST>(a, smem);
 }
 
@@ -587,7 +591,11 @@ DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
   X(10, 10, 3, 1, false, 0)   \
   X(10, 10, 4, 1, false, 0)
 
-// every stage placed on one GPU, one workgroup each (blockIdx.x = local stage)
+// every stage placed on one GPU, one workgroup each (blockIdx.x = local stage).  One
+// kernel holds the bodies of every stage shape of at most MAXNL layers: its registers are
+// allocated for the largest of them, so the 4- and 5-layer bodies (which need all 512
+// and spill) get their own instance and a launch of shorter stages never pays for them.
+template <int MAXNL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void split_multi_kernel(DtpSplitLaunch) {
   __shared__ __align__(16) unsigned char smem[kSplitSmemBytes];
   const int b = blockIdx.x;
@@ -597,8 +605,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int shape = L->shape_id[b];
   const DtpSplitStageArgs a = L->stage[b];
   int id = 0;
-#define X(I, H, N, O, F, FI)                                                                \
-  if (shape == id) split_stage_body<Stage<I, H, N, O, F>, (bool)FI, !F>(a, smem); \
+#define X(I, H, N, O, F, FI)                                                                        \
+  if constexpr (N <= MAXNL) {                                                                       \
+    if (shape == id) split_stage_body<Stage<I, H, N, O, F>, (bool)FI, !F>(a, smem);                 \
+  }                                                                                                 \
   ++id;
   DTP_SPLIT_SHAPES(X)
 #undef X
@@ -659,14 +669,22 @@ int dtp_split_launch(const DtpSplitLaunch* L, void* stream) {
       DTP_SPLIT_SHAPES(X)
 #undef X
   };
+  static const int layers_of[] = {
+#define X(I, H, N, O, F, FI) N,
+      DTP_SPLIT_SHAPES(X)
+#undef X
+  };
+  int maxnl = 0;
   constexpr int nshapes = sizeof(first_of) / sizeof(first_of[0]);
   for (int i = 0; i < L->n; ++i) {
     const int id = L->shape_id[i];
     if (id < 0 || id >= nshapes) return set_err(-2, "split launch: stage shape not instantiated");
     if (int rc = validate_stage(&L->stage[i], first_of[id], last_of[id])) return rc;
     if (L->stage[i].n_steps != L->stage[0].n_steps) return set_err(-1, "split launch: stages disagree on n_steps");
+    maxnl = layers_of[id] > maxnl ? layers_of[id] : maxnl;
   }
-  hipLaunchKernelGGL(dtp::split_multi_kernel, dim3(L->n), dim3(dtp::kBlock), 0, (hipStream_t)stream, *L);
+  if (maxnl <= 3) hipLaunchKernelGGL(dtp::split_multi_kernel<3>, dim3(L->n), dim3(dtp::kBlock), 0, (hipStream_t)stream, *L);
+  else hipLaunchKernelGGL(dtp::split_multi_kernel<5>, dim3(L->n), dim3(dtp::kBlock), 0, (hipStream_t)stream, *L);
   return dtp::check_launch("split_multi_kernel");
 }
 

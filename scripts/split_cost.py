@@ -36,7 +36,7 @@ def run(K, local, launch="per_device", n=2000):
 
 if __name__ == "__main__":
     for K, local, launch in [(1, True, "per_device"), (2, True, "per_device"), (2, False, "per_device"),
-                             (2, True, "per_stage"), (5, True, "per_device"), (5, False, "per_device"),
+                             (2, True, "per_stage"), (3, True, "per_device"), (5, True, "per_device"),
                              (1, True, "per_device"), (2, True, "per_device")]:
-        print(json.dumps({"K": K, "links": "device" if local else "system", "launch": launch,
+        print(json.dumps({"lib": os.environ.get("DTP_LIB", "default"), "K": K, "links": "device" if local else "system", "launch": launch,
                           "us_per_step": round(run(K, local, launch), 3)}), flush=True)
