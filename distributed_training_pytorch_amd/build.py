@@ -178,9 +178,15 @@ def asm(src_name: str, out_dir: Path | None = None) -> Path:
 
 
 if __name__ == "__main__":
-    # python -m distributed_training_pytorch_amd.build [-v] [--variant NAME FLAG...]
+    # python -m distributed_training_pytorch_amd.build [-v] [--variant NAME [--sources a.hip,b.hip] FLAG...]
     if "--variant" in sys.argv:
         i = sys.argv.index("--variant")
-        print(variant(sys.argv[i + 1], sys.argv[i + 2:], verbose="-v" in sys.argv))
+        rest = [x for x in sys.argv[i + 2:] if x != "-v"]
+        srcs = ("mlp_train.hip",)
+        if "--sources" in rest:
+            j = rest.index("--sources")
+            srcs = tuple(rest[j + 1].split(","))
+            rest = rest[:j] + rest[j + 2:]
+        print(variant(sys.argv[i + 1], rest, srcs, verbose="-v" in sys.argv))
     else:
         print(build(verbose="-v" in sys.argv))

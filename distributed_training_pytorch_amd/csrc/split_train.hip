@@ -329,6 +329,23 @@ DTP_DEV void split_stage_body_v1(const DtpSplitStageArgs& a, unsigned char* smem
 // layer's weight block streams in during the current layer, the dW MFMA K-steps ride
 // between the input-gradient rows (mlp_pipe.h).  Same protocol, sampler, exchange and
 // optimizer as split_stage_body_v1 (the one-layer stages keep that one).
+#ifndef DTP_SPLIT_PROF
+#define DTP_SPLIT_PROF 0  // 1 (diagnostic builds only): s_memtime phase stamps of the first 8 steps, lane 0 of
+                          // wave 0 of the LAST stage, as u64 at float offset 32768 of its loss log
+#endif
+#define SPLIT_STAMP(K)                                                                            \
+  do {                                                                                            \
+    if constexpr (DTP_SPLIT_PROF && LAST) {                                                       \
+      if (tid == 0 && it < 8 && a.loss_log) {                                                     \
+        unsigned long long _t;                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");             \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        reinterpret_cast<unsigned long long*>(a.loss_log + 32768)[it * 16 + (K)] = _t;           \
+      }                                                                                           \
+    }                                                                                             \
+  } while (0)
+
 template <class S, bool FIRST, bool LAST>
 DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* smem) {
   using SC = Scal<S>;
@@ -417,6 +434,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
   float* const stg_hid = &sm.stage[wave][SplitPipeSmem<S>::AREAS - 1][0];
 
   for (int it = 0; it < a.n_steps; ++it) {
+    SPLIT_STAMP(0);
     const int t = t0 + it;
     const unsigned ep = (unsigned)t + 1u;
     const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
@@ -438,6 +456,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     } else {
       link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead, prev_local);
     }
+    SPLIT_STAMP(1);
     BBlk<S, NL - 1> pbt;
     TopB2<S> pbt2;
     {
@@ -446,6 +465,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       pipe_forward<S, 0>(sm.wb, pb0, h, slope, pbt, pbt2);
     }
     // ---- output gradient: from the next stage, or the MSE loss (last stage)
+    SPLIT_STAMP(2);
     float dz[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) dz[j] = 0.f;
@@ -472,6 +492,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     f32x4 acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    SPLIT_STAMP(3);
     const PipeBwdCtx<S> pc{sm.wb, stg_pack, stg_hid, lane, slope, lpart};
     if constexpr (NL >= 3) {
       pipe_backward<S>(pc, pbt, pbt2, h, dz, acc);
@@ -495,6 +516,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       });
       link_send<S::IN>(a.grad_out, tid, ep, dx, valid, prev_local);
     }
+    SPLIT_STAMP(4);
     // ---- each wave parks its partial tiles in its own staging area (its staging reads
     // were issued before these writes); one barrier publishes them
     {
@@ -505,6 +527,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
         for (int r = 0; r < 4; ++r) stg_pack[tt * 256 + (4 * q + r) * 16 + col] = acc[tt][r];
     }
     __syncthreads();
+    SPLIT_STAMP(5);
     float g[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
@@ -521,8 +544,10 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
         ls += sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
       loss = ls * inv;
     }
+    SPLIT_STAMP(6);
     float gloss = loss;
     if (use_dp) gloss = xgmi_allreduce_slots<NPT>(dp, 0, P, g, loss, ep, tid);
+    SPLIT_STAMP(7);
     // ---- optimizer (registers) + weight refresh (LDS)
     const float gs = a.hp.grad_scale;
     if (adam) {
@@ -544,7 +569,9 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       const int owner = use_dp ? xgmi_loss_tid<NPT>(P, kBlock) : 0;
       if (tid == owner && a.loss_log) a.loss_log[t % a.loss_log_cap] = use_dp ? gloss * gs : loss;
     }
+    SPLIT_STAMP(8);
     __syncthreads();  // new weights visible; reduction tiles consumed before the next staging writes
+    SPLIT_STAMP(9);
     if (adam && (it + 1) % kSplitAdamTab == 0 && it + 1 < a.n_steps) {
       fill_adam(it + 1);
       __syncthreads();
