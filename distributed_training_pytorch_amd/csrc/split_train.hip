@@ -184,7 +184,39 @@ DTP_DEV void split_stage_body_v1(const DtpSplitStageArgs& a, unsigned char* smem
       return tid < bp.size ? sample_index(smp, bp, keys, tid) : 0;
     }
   };
-  int di_next = index_at(epoch, bi);
+  // the sample pipeline (as the fused step's FAST instance): step t's inputs / targets are
+  // gathered from LDS at the end of step t-1, from a dataset index loaded a whole step
+  // before that -- so no step waits on a global load (a wait at the loop head would also
+  // wait out the previous step's loss-log store)
+  int e2 = epoch, b2 = bi;
+  auto roll2 = [&]() {
+    if (++b2 == smp.steps_per_epoch) {
+      b2 = 0;
+      ++e2;
+    }
+  };
+  float nx[S::IN], ny[S::OUT];
+  auto gather = [&](int di_) {
+    di_ = (unsigned)di_ < (unsigned)smp.n ? di_ : 0;  // never index out of range
+    if constexpr (FIRST)
+      static_for<0, S::IN>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        nx[i] = cached ? sm.data[di_ * S::IN + i] : a.X[(size_t)di_ * S::IN + i];
+      });
+    if constexpr (LAST)
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        ny[j] = cached ? sm.data[smp.n * XW + di_ * S::OUT + j] : a.Y[(size_t)di_ * S::OUT + j];
+      });
+  };
+  int di_next = 0;
+  if constexpr (FIRST || LAST) {
+    const int d0 = index_at(e2, b2);
+    roll2();
+    di_next = index_at(e2, b2);  // step t0 + 1
+    roll2();
+    gather(d0);
+  }
   auto fill_adam = [&](int base) {
     const int n = min(kSplitAdamTab, a.n_steps - base);
     for (int e = tid; e < n; e += kBlock) {
@@ -213,19 +245,16 @@ DTP_DEV void split_stage_body_v1(const DtpSplitStageArgs& a, unsigned char* smem
     const unsigned ep = (unsigned)t + 1u;
     const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
     const bool valid = tid < bsz;
-    const int di = di_next;
-    // the next step's cursor and index request (consumed one step later)
     if (++bi == smp.steps_per_epoch) {
       bi = 0;
       ++epoch;
     }
-    if (it + 1 < a.n_steps) di_next = index_at(epoch, bi);
     // ---- forward
     float h[NL + 1][16];
     if constexpr (FIRST) {
       static_for<0, S::IN>([&](auto IC) {
         constexpr int i = decltype(IC)::value;
-        h[0][i] = valid ? (cached ? sm.data[di * S::IN + i] : a.X[(size_t)di * S::IN + i]) : 0.f;
+        h[0][i] = valid ? nx[i] : 0.f;
       });
     } else {
       link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead, prev_local);
@@ -250,7 +279,7 @@ DTP_DEV void split_stage_body_v1(const DtpSplitStageArgs& a, unsigned char* smem
       float lpart = 0.f;
       static_for<0, S::OUT>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        const float y = valid ? (cached ? sm.data[smp.n * XW + di * S::OUT + j] : a.Y[(size_t)di * S::OUT + j]) : 0.f;
+        const float y = valid ? ny[j] : 0.f;
         const float d = h[NL][j] - y;
         lpart = valid ? fmaf(d, d, lpart) : lpart;
         dz[j] = valid ? 2.f * d * inv : 0.f;
@@ -280,6 +309,11 @@ DTP_DEV void split_stage_body_v1(const DtpSplitStageArgs& a, unsigned char* smem
     // ---- data parallel: this stage's gradient (+ loss) summed over the ranks
     float gloss = loss;
     if (use_dp) gloss = xgmi_allreduce_slots<NPT>(dp, 0, P, g, loss, ep, tid);
+    if constexpr (FIRST || LAST) {  // the next step's sample, and the index of the one after it
+      gather(di_next);
+      di_next = index_at(e2, b2);
+      roll2();
+    }
 
     // ---- optimizer (registers) + weight refresh (LDS)
     const float gs = a.hp.grad_scale;
@@ -404,7 +438,39 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       return tid < bp.size ? sample_index(smp, bp, keys, tid) : 0;
     }
   };
-  int di_next = index_at(epoch, bi);
+  // the sample pipeline (as the fused step's FAST instance): step t's inputs / targets are
+  // gathered from LDS at the end of step t-1, from a dataset index loaded a whole step
+  // before that -- so no step waits on a global load (a wait at the loop head would also
+  // wait out the previous step's loss-log store)
+  int e2 = epoch, b2 = bi;
+  auto roll2 = [&]() {
+    if (++b2 == smp.steps_per_epoch) {
+      b2 = 0;
+      ++e2;
+    }
+  };
+  float nx[S::IN], ny[S::OUT];
+  auto gather = [&](int di_) {
+    di_ = (unsigned)di_ < (unsigned)smp.n ? di_ : 0;  // never index out of range
+    if constexpr (FIRST)
+      static_for<0, S::IN>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        nx[i] = cached ? sm.data[di_ * S::IN + i] : a.X[(size_t)di_ * S::IN + i];
+      });
+    if constexpr (LAST)
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        ny[j] = cached ? sm.data[smp.n * XW + di_ * S::OUT + j] : a.Y[(size_t)di_ * S::OUT + j];
+      });
+  };
+  int di_next = 0;
+  if constexpr (FIRST || LAST) {
+    const int d0 = index_at(e2, b2);
+    roll2();
+    di_next = index_at(e2, b2);  // step t0 + 1
+    roll2();
+    gather(d0);
+  }
   auto fill_adam = [&](int base) {
     const int n = min(kSplitAdamTab, a.n_steps - base);
     for (int e = tid; e < n; e += kBlock) {
@@ -439,19 +505,17 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     const unsigned ep = (unsigned)t + 1u;
     const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
     const bool valid = tid < bsz;
-    const int di = di_next;
     if (++bi == smp.steps_per_epoch) {
       bi = 0;
       ++epoch;
     }
-    if (it + 1 < a.n_steps) di_next = index_at(epoch, bi);
     const float inv = 1.f / (float)(bsz * S::OUT);
     // ---- forward (the first block is read here; the others stream in layer by layer)
     float h[NL + 1][16];
     if constexpr (FIRST) {
       static_for<0, S::IN>([&](auto IC) {
         constexpr int i = decltype(IC)::value;
-        h[0][i] = valid ? (cached ? sm.data[di * S::IN + i] : a.X[(size_t)di * S::IN + i]) : 0.f;
+        h[0][i] = valid ? nx[i] : 0.f;
       });
     } else {
       link_recv<S::IN>(a.act_in, tid, ep, h[0], valid, a.status, a.timeout_us, link_dead, prev_local);
@@ -482,7 +546,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     } else {
       static_for<0, S::OUT>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        const float y = valid ? (cached ? sm.data[smp.n * XW + di * S::OUT + j] : a.Y[(size_t)di * S::OUT + j]) : 0.f;
+        const float y = valid ? ny[j] : 0.f;
         const float d = h[NL][j] - y;
         lpart = valid ? fmaf(d, d, lpart) : lpart;
         dz[j] = valid ? 2.f * d * inv : 0.f;
@@ -547,6 +611,11 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     SPLIT_STAMP(6);
     float gloss = loss;
     if (use_dp) gloss = xgmi_allreduce_slots<NPT>(dp, 0, P, g, loss, ep, tid);
+    if constexpr (FIRST || LAST) {  // the next step's sample, and the index of the one after it
+      gather(di_next);
+      di_next = index_at(e2, b2);
+      roll2();
+    }
     SPLIT_STAMP(7);
     // ---- optimizer (registers) + weight refresh (LDS)
     const float gs = a.hp.grad_scale;
