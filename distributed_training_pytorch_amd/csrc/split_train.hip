@@ -115,9 +115,9 @@ struct SplitSmem {
 template <class S>
 struct SplitPipeSmem {
   static constexpr int AREAS = Scal<S>::PACK ? 2 : 1;
-  float wb[Scal<S>::LW];
-  float w0r[S::dout(0) * S::pad4(S::IN)];
-  float stage[kBlock / kWave][AREAS][2 * kStgArr];
+  alignas(16) float wb[Scal<S>::LW];
+  alignas(16) float w0r[S::dout(0) * S::pad4(S::IN)];
+  alignas(16) float stage[kBlock / kWave][AREAS][2 * kStgArr];
   float data[kSplitCache];
   float2 adam_tab[kSplitAdamTab];
 };
@@ -569,14 +569,33 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       __builtin_amdgcn_wave_barrier();
     }
     if constexpr (!FIRST) {  // dz now holds layer 0's output gradient: dx = W_0^T dz
-      float dx[16];
-      static_for<0, S::IN>([&](auto IC) { dx[decltype(IC)::value] = 0.f; });
-      static_for<0, S::dout(0)>([&](auto JC) {
+      // the whole row-major block in flight at once (broadcast ds_read_b128; LDS returns in
+      // order), then output-major pair FMAs: the order of every sum is j ascending
+      constexpr int NQ = IP0 / 4, O0 = S::dout(0);
+      float4 w4[O0][NQ];
+      static_for<0, O0>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        static_for<0, S::IN>([&](auto IC) {
-          constexpr int i = decltype(IC)::value;
-          dx[i] = fmaf(sm.w0r[j * IP0 + i], dz[j], dx[i]);
+        static_for<0, NQ>([&](auto QC) {
+          constexpr int q = decltype(QC)::value;
+          w4[j][q] = row_quad<S::IN, q>(sm.w0r + j * IP0);
         });
+      });
+      f32x2 gx[2 * NQ];
+      static_for<0, 2 * NQ>([&](auto QC) { gx[decltype(QC)::value] = f32x2{0.f, 0.f}; });
+      static_for<0, O0>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const f32x2 d = f32x2{dz[j], dz[j]};
+        static_for<0, NQ>([&](auto QC) {
+          constexpr int q = decltype(QC)::value;
+          if constexpr (4 * q < S::IN) gx[2 * q] = __builtin_elementwise_fma(f32x2{w4[j][q].x, w4[j][q].y}, d, gx[2 * q]);
+          if constexpr (4 * q + 2 < S::IN)
+            gx[2 * q + 1] = __builtin_elementwise_fma(f32x2{w4[j][q].z, w4[j][q].w}, d, gx[2 * q + 1]);
+        });
+      });
+      float dx[16];
+      static_for<0, S::IN>([&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        dx[i] = (i & 1) ? gx[i / 2].y : gx[i / 2].x;
       });
       link_send<S::IN>(a.grad_out, tid, ep, dx, valid, prev_local);
     }
