@@ -115,8 +115,10 @@ struct SplitSmem {
 template <class S>
 struct SplitPipeSmem {
   static constexpr int AREAS = Scal<S>::PACK ? 2 : 1;
-  alignas(16) float wb[Scal<S>::LW];
-  alignas(16) float w0r[S::dout(0) * S::pad4(S::IN)];
+  // one float past each block: the sink the non-owning slots' scatter stores land in
+  static constexpr int WB_SINK = Scal<S>::LW, W0R_SINK = S::dout(0) * S::pad4(S::IN);
+  alignas(16) float wb[WB_SINK + 4];
+  alignas(16) float w0r[W0R_SINK + 4];
   alignas(16) float stage[kBlock / kWave][AREAS][2 * kStgArr];
   float data[kSplitCache];
   float2 adam_tab[kSplitAdamTab];
@@ -412,10 +414,19 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     // layer-0 weights, row-major: the input gradient of a non-first stage
     const int q = p - S::gw(0);
     p0r[k] = (!FIRST && own && q >= 0 && q < S::gb(0)) ? (q / S::IN) * IP0 + q % S::IN : -1;
+    // branch-free weight refresh: a slot without a copy in a block stores to its sink
+    // (the fused step's idiom; the optimizer also runs on the non-owned slots: their
+    // state is zeros / never stored)
+    pfl[k] = pfl[k] >= 0 ? pfl[k] : SplitPipeSmem<S>::WB_SINK;
+    pb[k] = pb[k] >= 0 ? pb[k] : SplitPipeSmem<S>::WB_SINK;
+    p0r[k] = p0r[k] >= 0 ? p0r[k] : SplitPipeSmem<S>::W0R_SINK;
   }
   for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   for (int e = tid; e < S::dout(0) * IP0; e += kBlock) sm.w0r[e] = 0.f;
-  const bool cached = a.cache_data && smp.n * (XW + YW) <= kSplitCache;
+  // the dataset is in LDS (split_stage_body sends uncached runs to the round-3 body): the
+  // sample gather is straight-line LDS code -- a global-load path beside it made the
+  // compiler wait out every outstanding store (links, loss log) before each gather
+  constexpr bool cached = true;
   if (cached) {
     if constexpr (FIRST)
       for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
@@ -483,9 +494,9 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
   auto scatter = [&]() {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      if (pfl[k] >= 0) sm.wb[pfl[k]] = pw[k];
-      if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
-      if (p0r[k] >= 0) sm.w0r[p0r[k]] = pw[k];
+      sm.wb[pfl[k]] = pw[k];
+      sm.wb[pb[k]] = pw[k];
+      if constexpr (!FIRST) sm.w0r[p0r[k]] = pw[k];
     }
   };
   __syncthreads();  // pads zeroed before the owners scatter
@@ -644,13 +655,11 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       as.step_size = sc.x;
       as.bc2_sqrt = sc.y;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k)
-        if (pfl[k] >= 0) adam_update(pw[k], mr[k], vr[k], g[k] * gs, as);
+      for (int k = 0; k < NPT; ++k) adam_update(pw[k], mr[k], vr[k], g[k] * gs, as);
     } else {
       const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k)
-        if (pfl[k] >= 0) sgd_update(pw[k], mr[k], g[k] * gs, lr, mom, wd, t == 0);
+      for (int k = 0; k < NPT; ++k) sgd_update(pw[k], mr[k], g[k] * gs, lr, mom, wd, t == 0);
     }
     scatter();
     if constexpr (LAST) {
@@ -683,8 +692,15 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
 
 template <class S, bool FIRST, bool LAST>
 DTP_DEV void split_stage_body(const DtpSplitStageArgs& a, unsigned char* smem) {
-  if constexpr (DTP_SPLIT_PIPE && S::NL >= 2) split_stage_body_pipe<S, FIRST, LAST>(a, smem);
-  else split_stage_body_v1<S, FIRST, LAST>(a, smem);
+  constexpr int XW = FIRST ? S::IN : 0, YW = LAST ? S::OUT : 0;
+  const bool cached = a.cache_data && a.smp.n * (XW + YW) <= kSplitCache;
+  if constexpr (DTP_SPLIT_PIPE && S::NL >= 2) {
+    if (cached) {
+      split_stage_body_pipe<S, FIRST, LAST>(a, smem);
+      return;
+    }
+  }
+  split_stage_body_v1<S, FIRST, LAST>(a, smem);
 }
 
 // (IN, H, NL, OUT, FINAL_ACT, FIRST): the contiguous layer ranges of the toy model

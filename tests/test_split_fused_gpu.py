@@ -27,16 +27,16 @@ def _init(seed=5):
     return torch.randn(TOY_SPEC.P, generator=torch.Generator().manual_seed(seed)) * 0.4
 
 
-def _engine(K, ocfg, bounds=None, batch=256, world=1, rank=0, seed=11, **kw):
-    ds = ToyData(n=512, seed=2)
-    geom = SamplerGeometry(n=512, world=world, rank=rank, batch=batch, seed=seed)
+def _engine(K, ocfg, bounds=None, batch=256, world=1, rank=0, seed=11, n=512, **kw):
+    ds = ToyData(n=n, seed=2)
+    geom = SamplerGeometry(n=n, world=world, rank=rank, batch=batch, seed=seed)
     return FusedLayerSplit(TOY_SPEC, [DEV] * K, ds.X, ds.Y, geom, ocfg, _init(), boundaries=bounds, **kw), ds
 
 
-def _reference(ocfg, steps, batch=256, world=1, seed=11):
-    ds = ToyData(n=512, seed=2)
+def _reference(ocfg, steps, batch=256, world=1, seed=11, n=512):
+    ds = ToyData(n=n, seed=2)
     # the engine's default order: the reference's DistributedSampler (randperm per epoch)
-    geoms = [EpochIndexStream(SamplerGeometry(n=512, world=world, rank=r, batch=batch, seed=seed))
+    geoms = [EpochIndexStream(SamplerGeometry(n=n, world=world, rank=r, batch=batch, seed=seed))
              for r in range(world)]
     p, l = torch_train(TOY_SPEC, [_init()], ds.X, ds.Y, geoms, steps, ocfg, "mse")
     return p[0], l[:, 0]
@@ -66,6 +66,22 @@ def test_fused_split_partial_batches_and_epochs():
     eng.train(steps)
     eng.synchronize()
     rp, rl = _reference(ocfg, steps, batch=100)
+    torch.testing.assert_close(eng.losses(0, steps), rl, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(eng.flat_params_cpu(), rp, rtol=1e-4, atol=2e-5)
+    eng.close()
+
+
+@pytest.mark.parametrize("K", [1, 2])
+def test_fused_split_dataset_past_lds_cache(K):
+    """4096 samples x (2 inputs + 1 target) floats exceed the stage's LDS data cache
+    (8192 floats) on the whole-model stage: that stage gathers from global memory
+    through the round-3 body, the cached stages through the pipelined one."""
+    ocfg = OptimConfig(lr=1e-2)
+    steps = 10
+    eng, _ = _engine(K, ocfg, n=4096)
+    eng.train(steps)
+    eng.synchronize()
+    rp, rl = _reference(ocfg, steps, n=4096)
     torch.testing.assert_close(eng.losses(0, steps), rl, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(eng.flat_params_cpu(), rp, rtol=1e-4, atol=2e-5)
     eng.close()
