@@ -61,12 +61,35 @@ DTP_DEV AdamScalars adam_consts(const DtpHyper& hp) {
 // each update is fixed by the source, not by how the compiler scheduled the
 // surrounding kernel: every kernel instance (FAST or generic, fused step or flat
 // optimizer) produces bitwise the same update.
+// DTP_ADAM_FAST (default): sqrt(v) from the hardware square root, and each division as
+// a reciprocal estimate, a product and one residual correction (fma) -- within an ulp or
+// two of the correctly rounded results (the torch.optim.Adam comparisons of the GPU tests
+// hold at their tolerances, down to rtol 1e-6 for the flat optimizer), and a short
+// dependency chain: the precise forms (v_div_scale / fmas / fixup, the scaled sqrt
+// refinement) were ~30 dependent VALU ops per parameter and 0.16 us of the 4.3 us fused
+// step (profiles/r4_adam/).  -DDTP_ADAM_FAST=0 restores torch's exact division / sqrt.
+#ifndef DTP_ADAM_FAST
+#define DTP_ADAM_FAST 1
+#endif
+
+// a / b for a normal, positive b: reciprocal estimate, product, one residual correction
+DTP_DEV float div_nr(float a, float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  const float q = a * r;
+  return fmaf(fmaf(-b, q, a), r, q);
+}
+
 DTP_DEV void adam_update(float& p, float& m, float& v, float g, const AdamScalars& s) {
   if (s.wd != 0.f) g = fmaf(s.wd, p, g);
   m = fmaf(s.one_m_b1, g - m, m);                  // m.lerp_(g, 1 - b1)
   v = fmaf(s.one_m_b2 * g, g, v * s.b2);           // v.mul_(b2).addcmul_(g, g, 1 - b2)
+#if DTP_ADAM_FAST
+  const float denom = div_nr(__builtin_amdgcn_sqrtf(v), s.bc2_sqrt) + s.eps;
+  p = fmaf(-s.step_size, div_nr(m, denom), p);
+#else
   const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;
   p = fmaf(-s.step_size, m / denom, p);            // p.addcdiv_(m, denom, -step_size)
+#endif
 }
 
 DTP_DEV void sgd_update(float& p, float& buf, float g, float lr, float mom, float wd, bool first) {
