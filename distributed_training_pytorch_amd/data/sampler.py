@@ -358,6 +358,10 @@ class PermutationRing:
         self.hi = max(self.hi, e0 + count - 1)
         self.lo = max(self.lo, self.hi - self.E + 1)
 
+    def needs_write(self, e_lo: int, e_hi: int) -> bool:
+        """Would :meth:`ensure` copy into the table (and so overwrite slots)?"""
+        return e_lo < self.lo or e_hi > self.hi
+
     def ensure(self, e_lo: int, e_hi: int) -> None:
         if e_hi - e_lo + 1 > self.E:
             raise ValueError(f"a launch spanning {e_hi - e_lo + 1} epochs exceeds the {self.E}-epoch ring: "

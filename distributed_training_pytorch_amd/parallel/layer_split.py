@@ -438,6 +438,11 @@ class FusedLayerSplit:
             else:
                 self.streams[k] = torch.cuda.Stream(device=dev)
         self.t = 0
+        # devices whose split streams must wait for host-side state edits queued on the
+        # current stream (construction synchronizes; load_state_dict / ring refills mark)
+        self._dirty: set = set()
+        self._copy_stream = None  # loss read-back, off the split streams' critical path
+        self._copy_guard = None  # (event, first step) of the last read-back still reading loss slots
         self._launch = {}
         for key, stages in self.groups.items():
             dev = self.key_dev[key]
@@ -485,27 +490,49 @@ class FusedLayerSplit:
 
     def train(self, n_steps: int) -> None:
         """n_steps iterations: ONE persistent launch per GPU (its stages as co-resident
-        workgroups), asynchronous."""
+        workgroups), asynchronous.  Back-to-back calls queue on the split streams with no
+        cross-stream wait unless something shared was rewritten in between."""
         if n_steps <= 0:
             return
         import ctypes
 
         for dev, ring in self.rings.items():
-            # the ring refill is a copy on dev's current stream: order it after the previous
-            # launches on the split streams, which may still read the slots it overwrites
-            for k, st in self.streams.items():
-                if self.key_dev[k] == dev:
-                    torch.cuda.current_stream(dev).wait_stream(st)
-            ring.ensure(*ring.epochs_of_steps(self.t, self.t + n_steps - 1))
+            e_lo, e_hi = ring.epochs_of_steps(self.t, self.t + n_steps - 1)
+            keys = [k for k in self.streams if self.key_dev[k] == dev]
+            if len(keys) == 1:
+                # the one stream that reads this ring refills it too: stream order keeps
+                # the copy behind the launches still reading the slots it overwrites
+                with torch.cuda.stream(self.streams[keys[0]]):
+                    ring.ensure(e_lo, e_hi)
+            elif ring.needs_write(e_lo, e_hi):
+                cur = torch.cuda.current_stream(dev)
+                for k in keys:
+                    cur.wait_stream(self.streams[k])
+                ring.ensure(e_lo, e_hi)
+                self._dirty.add(dev)
+            else:
+                ring.ensure(e_lo, e_hi)  # no copy; may start the next block's host generation
+        last_key = self._last_key()
+        cap = self.loss_log.shape[0]
         for key, L in self._launch.items():
             dev = self.key_dev[key]
             st = self.streams[key]
-            st.wait_stream(torch.cuda.current_stream(dev))  # after any host-side state edits
+            if dev in self._dirty:
+                st.wait_stream(torch.cuda.current_stream(dev))  # after the host-side state edits
+            if key == last_key and self._copy_guard is not None:
+                ev, c0 = self._copy_guard
+                if self.t + n_steps - c0 > cap:  # this launch's loss slots wrap onto unread ones
+                    st.wait_event(ev)
             for j in range(L.n):
                 L.stage[j].n_steps = n_steps
             with torch.cuda.device(dev):
                 nat.check(self.lib.dtp_split_launch(ctypes.byref(L), nat.stream_ptr(st)), "dtp_split_launch")
+        self._dirty.clear()
         self.t += n_steps
+
+    def _last_key(self):
+        """The launch that runs the last stage (it writes the loss log)."""
+        return next(k for k, v in self.groups.items() if len(self.devices) - 1 in v)
 
     def _join(self):
         for k, st in self.streams.items():
@@ -534,24 +561,29 @@ class FusedLayerSplit:
         return self.loss_log.index_select(0, ids.to(self.loss_log.device)).cpu()
 
     def losses_async(self, t0: int, t1: int):
-        """Pinned copy of the losses of steps [t0, t1) queued behind the last stage's
-        work; ``.wait()`` returns [[loss], ...] (the fused engine's LossReadback)."""
+        """Pinned copy of the losses of steps [t0, t1), queued on a copy stream behind the
+        last stage's launch; ``.wait()`` returns [[loss], ...] (the fused engine's
+        LossReadback).  The split streams never wait for it, unless a later launch's loss
+        slots wrap onto the ones it still reads."""
         from ..engine.fused_trainer import LossReadback
 
         dev = self.devices[-1]
-        cur = torch.cuda.current_stream(dev)
-        for k, st in self.streams.items():
-            if self.key_dev[k] == dev:
-                cur.wait_stream(st)
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(device=dev)
+        cs = self._copy_stream
+        cs.wait_stream(self.streams[self._last_key()])
         cap = self.loss_log.shape[0]
-        ids = torch.arange(max(t0, t1 - cap), t1) % cap
-        with torch.cuda.device(dev):
-            rows = self.loss_log.index_select(0, ids.to(dev)).view(-1, 1)
-            host = torch.empty(rows.shape, pin_memory=True)
-            host.copy_(rows, non_blocking=True)
+        t0 = max(t0, t1 - cap)
+        a, b = t0 % cap, t1 - t0
+        with torch.cuda.device(dev), torch.cuda.stream(cs):
+            src = (self.loss_log[a:a + b] if a + b <= cap
+                   else torch.cat([self.loss_log[a:], self.loss_log[:a + b - cap]]))
+            host = torch.empty(src.shape, pin_memory=True)
+            host.copy_(src, non_blocking=True)
             ev = torch.cuda.Event()
-            ev.record(cur)
-        return LossReadback(host, None, ev, self.rank)
+            ev.record(cs)
+        self._copy_guard = (ev, t0)
+        return LossReadback(host.view(-1, 1), None, ev, self.rank)
 
     def flat_params_cpu(self) -> torch.Tensor:
         self._join()
@@ -580,6 +612,7 @@ class FusedLayerSplit:
             self.step[s].fill_(int(sd["step"]))
             o += n
         self.t = int(sd["t"])
+        self._dirty.update(self.devices)  # the next launches wait for these copies
 
     def close(self):
         import ctypes

@@ -26,6 +26,7 @@ eng = FusedLayerSplit(TOY_SPEC, [dev] * K, ds.X, ds.Y, SamplerGeometry(n=512, ba
 eng.train(20)
 eng.synchronize()
 eng.loss_log.zero_()
+torch.cuda.synchronize(dev)  # the split streams do not wait on the current stream
 eng.train(8)
 eng.synchronize()
 st = eng.loss_log[32768:32768 + 8 * 16 * 2].view(torch.int64).view(8, 16).cpu()
