@@ -426,13 +426,10 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
   // the dataset is in LDS (split_stage_body sends uncached runs to the round-3 body): the
   // sample gather is straight-line LDS code -- a global-load path beside it made the
   // compiler wait out every outstanding store (links, loss log) before each gather
-  constexpr bool cached = true;
-  if (cached) {
-    if constexpr (FIRST)
-      for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
-    if constexpr (LAST)
-      for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * XW + e] = a.Y[e];
-  }
+  if constexpr (FIRST)
+    for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
+  if constexpr (LAST)
+    for (int e = tid; e < smp.n * S::OUT; e += kBlock) sm.data[smp.n * XW + e] = a.Y[e];
   const int t0 = a.step[0];
   int epoch = t0 / smp.steps_per_epoch;
   int bi = t0 - epoch * smp.steps_per_epoch;
@@ -466,12 +463,12 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
     if constexpr (FIRST)
       static_for<0, S::IN>([&](auto IC) {
         constexpr int i = decltype(IC)::value;
-        nx[i] = cached ? sm.data[di_ * S::IN + i] : a.X[(size_t)di_ * S::IN + i];
+        nx[i] = sm.data[di_ * S::IN + i];
       });
     if constexpr (LAST)
       static_for<0, S::OUT>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        ny[j] = cached ? sm.data[smp.n * XW + di_ * S::OUT + j] : a.Y[(size_t)di_ * S::OUT + j];
+        ny[j] = sm.data[smp.n * XW + di_ * S::OUT + j];
       });
   };
   int di_next = 0;
