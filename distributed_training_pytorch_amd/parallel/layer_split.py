@@ -442,7 +442,7 @@ class FusedLayerSplit:
         # current stream (construction synchronizes; load_state_dict / ring refills mark)
         self._dirty: set = set()
         self._copy_stream = None  # loss read-back, off the split streams' critical path
-        self._copy_guard = None  # (event, first step) of the last read-back still reading loss slots
+        self._copy_guards: list = []  # (event, first step) of the read-backs that may still read loss slots
         self._launch = {}
         for key, stages in self.groups.items():
             dev = self.key_dev[key]
@@ -519,10 +519,11 @@ class FusedLayerSplit:
             st = self.streams[key]
             if dev in self._dirty:
                 st.wait_stream(torch.cuda.current_stream(dev))  # after the host-side state edits
-            if key == last_key and self._copy_guard is not None:
-                ev, c0 = self._copy_guard
-                if self.t + n_steps - c0 > cap:  # this launch's loss slots wrap onto unread ones
-                    st.wait_event(ev)
+            if key == last_key:
+                self._copy_guards = [(ev, c0) for ev, c0 in self._copy_guards if not ev.query()]
+                for ev, c0 in self._copy_guards:
+                    if self.t + n_steps - c0 > cap:  # this launch's loss slots wrap onto unread ones
+                        st.wait_event(ev)
             for j in range(L.n):
                 L.stage[j].n_steps = n_steps
             with torch.cuda.device(dev):
@@ -582,7 +583,7 @@ class FusedLayerSplit:
             host.copy_(src, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(cs)
-        self._copy_guard = (ev, t0)
+        self._copy_guards.append((ev, t0))
         return LossReadback(host.view(-1, 1), None, ev, self.rank)
 
     def flat_params_cpu(self) -> torch.Tensor:

@@ -87,6 +87,23 @@ def test_fused_split_dataset_past_lds_cache(K):
     eng.close()
 
 
+def test_fused_split_loss_readback_across_a_small_log_ring():
+    """A 16-slot loss ring and 8-step launches: launch k+2 rewrites the slots read-back k
+    reads, so it must wait for that copy (and only for that one)."""
+    ocfg = OptimConfig(lr=1e-2)
+    eng, _ = _engine(2, ocfg, log_cap=16)
+    handles = []
+    for _ in range(5):
+        t0 = eng.t
+        eng.train(8)
+        handles.append(eng.losses_async(t0, t0 + 8))
+    got = torch.tensor([r[0] for h in handles for r in h.wait()])
+    eng.synchronize()
+    _, rl = _reference(ocfg, 40)
+    torch.testing.assert_close(got, rl, rtol=1e-4, atol=1e-5)
+    eng.close()
+
+
 def test_fused_split_step_time():
     """The reference's 2-GPU split at batch 256, both stages on one GPU: the whole
     iteration (2 hand-offs + both stages' fwd/bwd/Adam) in microseconds, not the
