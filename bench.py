@@ -21,6 +21,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -194,12 +195,17 @@ def main():
     xstats = a.impl == "native" and world > 1 and runner.comm == "xgmi"
     if xstats:
         runner.exchange_stats_reset()  # stream-ordered, covered by the synchronize below
+    # no cyclic-GC pass inside the timed region (a collection there is tens of us of
+    # host time on a sub-millisecond measurement); collected just before instead
+    gc.collect()
+    gc.disable()
     sync_barrier()
     sync()
     t0 = time.perf_counter()
     train(a.steps)
     sync_barrier()
     t1 = time.perf_counter()
+    gc.enable()
     elapsed = comm_util.all_reduce_scalar(t1 - t0, dist.ReduceOp.MAX)
     ms_per_step = 1e3 * elapsed / a.steps
     total_samples = comm_util.all_reduce_scalar(float(per_rank_batch * a.steps))
