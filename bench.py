@@ -79,12 +79,34 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_idle_ticks(cpus, window_s: float = 0.03) -> dict:
+    """Idle + iowait ticks of each CPU in ``cpus`` over ``window_s`` (/proc/stat); {} when
+    unreadable."""
+    def snap():
+        out = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    v = line.split()
+                    out[int(v[0][3:])] = int(v[4]) + int(v[5])
+        return out
+
+    try:
+        a = snap()
+        time.sleep(window_s)
+        b = snap()
+    except (OSError, ValueError, IndexError):
+        return {}
+    return {c: b[c] - a[c] for c in cpus if c in a and c in b}
+
+
 def pin_host_thread(dev) -> int | None:
     """Pin this (launching, synchronizing) thread to one CPU of the GPU's NUMA node: the
     K-step call is a launch, a wait and a synchronize, so a migration or a remote-node
     wakeup lands inside the timed region.  The CPU comes from the GPU's PCI
-    ``local_cpulist`` within this process's allowed set (each local rank takes its own);
-    None when the box does not expose it."""
+    ``local_cpulist`` within this process's allowed set, idlest first (each local rank
+    takes its own; DTP_BENCH_PIN=first: the first ones, 0: no pinning); None when the box
+    does not expose it."""
     if dev.type != "cuda" or not hasattr(os, "sched_setaffinity"):
         return None
     try:
@@ -96,6 +118,11 @@ def pin_host_thread(dev) -> int | None:
             lo, _, hi = part.partition("-")
             local.update(range(int(lo), int(hi or lo) + 1))
         allowed = sorted(local & os.sched_getaffinity(0)) or sorted(os.sched_getaffinity(0))
+        # the idlest CPUs first (other processes on a shared host pin threads too): idle
+        # time of each CPU over 30 ms of /proc/stat; ranks of one node take distinct picks
+        idle = cpu_idle_ticks(allowed) if os.environ.get("DTP_BENCH_PIN") != "first" else {}
+        if idle:
+            allowed = sorted(allowed, key=lambda c: -idle.get(c, 0))  # stable: ties keep CPU order
         cpu = allowed[int(os.environ.get("LOCAL_RANK", "0")) % len(allowed)]
         os.sched_setaffinity(0, {cpu})
         return cpu
