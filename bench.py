@@ -101,14 +101,16 @@ def cpu_idle_ticks(cpus, window_s: float = 0.03) -> dict:
 
 
 def pin_host_thread(dev) -> int | None:
-    """Pin this (launching, synchronizing) thread to one CPU of the GPU's NUMA node: the
-    K-step call is a launch, a wait and a synchronize, so a migration or a remote-node
-    wakeup lands inside the timed region.  The CPU comes from the GPU's PCI
-    ``local_cpulist`` within this process's allowed set, idlest first (each local rank
-    takes its own; DTP_BENCH_PIN=first: the first ones, 0: no pinning); None when the box
-    does not expose it."""
+    """Keep this (launching, synchronizing) thread on CPUs of the GPU's NUMA node: the
+    K-step call is a launch, a wait and a synchronize, so a remote-node wakeup lands
+    inside the timed region.  The CPUs come from the GPU's PCI ``local_cpulist`` within
+    this process's allowed set, idlest first over 30 ms of /proc/stat; each local rank
+    takes its own group of 4 (DTP_BENCH_PIN=one: a single CPU -- on a loaded shared host
+    that CPU's other work stalls the thread, profiles/r4_pin/; first: the first CPU; 0:
+    no pinning).  Returns the first CPU of the set, None when the box does not expose it."""
     if dev.type != "cuda" or not hasattr(os, "sched_setaffinity"):
         return None
+    mode = os.environ.get("DTP_BENCH_PIN", "set")
     try:
         pr = torch.cuda.get_device_properties(dev)
         bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
@@ -118,14 +120,14 @@ def pin_host_thread(dev) -> int | None:
             lo, _, hi = part.partition("-")
             local.update(range(int(lo), int(hi or lo) + 1))
         allowed = sorted(local & os.sched_getaffinity(0)) or sorted(os.sched_getaffinity(0))
-        # the idlest CPUs first (other processes on a shared host pin threads too): idle
-        # time of each CPU over 30 ms of /proc/stat; ranks of one node take distinct picks
-        idle = cpu_idle_ticks(allowed) if os.environ.get("DTP_BENCH_PIN") != "first" else {}
+        idle = cpu_idle_ticks(allowed) if mode != "first" else {}
         if idle:
             allowed = sorted(allowed, key=lambda c: -idle.get(c, 0))  # stable: ties keep CPU order
-        cpu = allowed[int(os.environ.get("LOCAL_RANK", "0")) % len(allowed)]
-        os.sched_setaffinity(0, {cpu})
-        return cpu
+        g = 1 if mode in ("one", "first") else min(4, len(allowed))
+        r = int(os.environ.get("LOCAL_RANK", "0"))
+        cpus = [allowed[(r * g + k) % len(allowed)] for k in range(g)]
+        os.sched_setaffinity(0, set(cpus))
+        return cpus[0]
     except (OSError, ValueError, AttributeError, IndexError):
         return None
 
@@ -151,7 +153,7 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
     dev = bootstrap.bind_device(env)
-    pinned = pin_host_thread(dev) if os.environ.get("DTP_BENCH_PIN", "1") != "0" else None
+    pinned = pin_host_thread(dev) if os.environ.get("DTP_BENCH_PIN", "set") != "0" else None
     if world > 1 or a.impl == "stock":  # the stock loop wraps its models in torch DDP even at W=1
         bootstrap.init_process_group(env, "gloo" if (a.share_gpu or dev.type == "cpu") else "nccl", dev)
     n = 512 * world if a.scaling == "weak" else 512
@@ -222,9 +224,9 @@ def main():
     xstats = a.impl == "native" and world > 1 and runner.comm == "xgmi"
     if xstats:
         runner.exchange_stats_reset()  # stream-ordered, covered by the synchronize below
-    # no cyclic-GC pass inside the timed region (a collection there is tens of us of
-    # host time on a sub-millisecond measurement); collected just before instead
-    gc.collect()
+    # no cyclic-GC pass inside the timed region.  (A gc.collect() right before it cost the
+    # first timed call ~40 us: the collection walks the whole heap and leaves the launch
+    # path's host caches cold; K=20 7.3-10.7 vs 5.3 us/step, profiles/r4_pin/k20_gc_ab.log.)
     gc.disable()
     sync_barrier()
     sync()
@@ -232,12 +234,20 @@ def main():
     train(a.steps)
     sync_barrier()
     t1 = time.perf_counter()
+    extra = []
+    for _ in range(int(os.environ.get("DTP_BENCH_EXTRA", "0"))):  # diagnostic: more timed calls, same recipe
+        sync_barrier()
+        sync()
+        u0 = time.perf_counter()
+        train(a.steps)
+        sync_barrier()
+        extra.append(round(1e3 * (time.perf_counter() - u0) / a.steps, 5))
     gc.enable()
     elapsed = comm_util.all_reduce_scalar(t1 - t0, dist.ReduceOp.MAX)
     ms_per_step = 1e3 * elapsed / a.steps
     total_samples = comm_util.all_reduce_scalar(float(per_rank_batch * a.steps))
     value = total_samples / elapsed
-    diag = {}
+    diag = {"extra_ms_per_step": extra} if extra else {}
     if world > 1 and a.impl == "native":
         # where a multi-GPU step goes (readable from the JSON line alone): the in-kernel
         # exchange's wait (publish -> last peer granule, per rank) and the rest of the step
