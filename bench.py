@@ -101,16 +101,16 @@ def cpu_idle_ticks(cpus, window_s: float = 0.03) -> dict:
 
 
 def pin_host_thread(dev) -> int | None:
-    """Keep this (launching, synchronizing) thread on CPUs of the GPU's NUMA node: the
+    """Keep this (launching, synchronizing) thread on a CPU of the GPU's NUMA node: the
     K-step call is a launch, a wait and a synchronize, so a remote-node wakeup lands
-    inside the timed region.  The CPUs come from the GPU's PCI ``local_cpulist`` within
+    inside the timed region.  The CPU comes from the GPU's PCI ``local_cpulist`` within
     this process's allowed set, idlest first over 30 ms of /proc/stat; each local rank
-    takes its own group of 4 (DTP_BENCH_PIN=one: a single CPU -- on a loaded shared host
-    that CPU's other work stalls the thread, profiles/r4_pin/; first: the first CPU; 0:
-    no pinning).  Returns the first CPU of the set, None when the box does not expose it."""
+    takes its own (DTP_BENCH_PIN=set: a group of 4; first: the first CPU; 0: no pinning;
+    A/Bs in profiles/r4_gpu/k20_pin_ab.jsonl.log and profiles/r4_pin/).  Returns the
+    first CPU of the set, None when the box does not expose it."""
     if dev.type != "cuda" or not hasattr(os, "sched_setaffinity"):
         return None
-    mode = os.environ.get("DTP_BENCH_PIN", "set")
+    mode = os.environ.get("DTP_BENCH_PIN", "one")
     try:
         pr = torch.cuda.get_device_properties(dev)
         bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
@@ -123,7 +123,7 @@ def pin_host_thread(dev) -> int | None:
         idle = cpu_idle_ticks(allowed) if mode != "first" else {}
         if idle:
             allowed = sorted(allowed, key=lambda c: -idle.get(c, 0))  # stable: ties keep CPU order
-        g = 1 if mode in ("one", "first") else min(4, len(allowed))
+        g = min(4, len(allowed)) if mode == "set" else 1
         r = int(os.environ.get("LOCAL_RANK", "0"))
         cpus = [allowed[(r * g + k) % len(allowed)] for k in range(g)]
         os.sched_setaffinity(0, set(cpus))
@@ -153,7 +153,7 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
     dev = bootstrap.bind_device(env)
-    pinned = pin_host_thread(dev) if os.environ.get("DTP_BENCH_PIN", "set") != "0" else None
+    pinned = pin_host_thread(dev) if os.environ.get("DTP_BENCH_PIN", "one") != "0" else None
     if world > 1 or a.impl == "stock":  # the stock loop wraps its models in torch DDP even at W=1
         bootstrap.init_process_group(env, "gloo" if (a.share_gpu or dev.type == "cpu") else "nccl", dev)
     n = 512 * world if a.scaling == "weak" else 512
