@@ -104,10 +104,11 @@ def pin_host_thread(dev) -> int | None:
     """Keep this (launching, synchronizing) thread on a CPU of the GPU's NUMA node: the
     K-step call is a launch, a wait and a synchronize, so a remote-node wakeup lands
     inside the timed region.  The CPU comes from the GPU's PCI ``local_cpulist`` within
-    this process's allowed set, idlest first over 30 ms of /proc/stat; each local rank
-    takes its own (DTP_BENCH_PIN=set: a group of 4; first: the first CPU; 0: no pinning;
-    A/Bs in profiles/r4_gpu/k20_pin_ab.jsonl.log and profiles/r4_pin/).  Returns the
-    first CPU of the set, None when the box does not expose it."""
+    this process's allowed set (one local process: idlest first over 30 ms of
+    /proc/stat); each local rank takes its own (DTP_BENCH_PIN=set: a group of 4; first:
+    the first CPU; 0: no pinning; A/Bs in profiles/r4_gpu/k20_pin_ab.jsonl.log and
+    profiles/r4_pin/).  Returns the first CPU of the set, None when the box does not
+    expose it."""
     if dev.type != "cuda" or not hasattr(os, "sched_setaffinity"):
         return None
     mode = os.environ.get("DTP_BENCH_PIN", "one")
@@ -120,7 +121,10 @@ def pin_host_thread(dev) -> int | None:
             lo, _, hi = part.partition("-")
             local.update(range(int(lo), int(hi or lo) + 1))
         allowed = sorted(local & os.sched_getaffinity(0)) or sorted(os.sched_getaffinity(0))
-        idle = cpu_idle_ticks(allowed) if mode != "first" else {}
+        # idlest first -- for a single local process only: ranks sampling /proc/stat at
+        # different moments would sort differently and could pick the same CPU
+        single = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) == 1
+        idle = cpu_idle_ticks(allowed) if mode != "first" and single else {}
         if idle:
             allowed = sorted(allowed, key=lambda c: -idle.get(c, 0))  # stable: ties keep CPU order
         g = min(4, len(allowed)) if mode == "set" else 1
