@@ -212,7 +212,13 @@ class BatchIndexer:
       device buffer by the native sampler kernel (``csrc/sampler.h``,
       ``dtp_sampler_indices``): no host index math and no host-to-device copy per
       step, stream-ordered with the steps that read them;
-    * exact torch order (``exact_torch``) or CPU: one vectorised epoch on the host,
+    * exact torch order (``exact_torch``) with shuffling on a GPU: the epoch
+      permutations come from a device ``PermutationRing`` (torch's randperm order, filled
+      by the native generator in blocks of epochs ahead of use); an epoch's per-rank list
+      is ONE device gather of the padded positions ``rank + k * world`` -- no host
+      permutation, list building or copy per epoch (it was ~50 us per step of the module
+      engine at 2 steps per epoch);
+    * otherwise (CPU, or unshuffled exact order): one vectorised epoch on the host,
       uploaded once per epoch (pinned, asynchronous).
     A returned tensor is a view that stays valid until ``block`` steps later.
     """
@@ -228,6 +234,12 @@ class BatchIndexer:
         self._epoch = -1
         self._ep_idx = None
         self._stream = EpochIndexStream(geom) if exact_torch else None
+        self._ring = None
+        if self.device.type == "cuda" and exact_torch and geom.distributed and geom.shuffle:
+            self._ring = PermutationRing(geom, self.device, kind="torch")
+            k = torch.arange(geom.num_samples, dtype=torch.int64)
+            # DistributedSampler: the permutation padded by repeating from its start, then [rank::world]
+            self._q = ((geom.rank + k * geom.world) % geom.n).to(self.device)
         if self.device.type == "cuda" and not exact_torch:
             from .. import _native as nat
 
@@ -249,6 +261,13 @@ class BatchIndexer:
                           "dtp_sampler_indices")
                 self._b0 = t
             return self._buf[t - self._b0, :size]
+        if self._ring is not None:
+            if epoch != self._epoch:
+                self._ring.ensure(epoch, epoch)  # stream-ordered refill when the ring runs out
+                perm = self._ring.table[epoch & (self._ring.E - 1)]
+                self._ep_idx = perm.index_select(0, self._q).long()
+                self._epoch = epoch
+            return self._ep_idx[start:start + size]
         if epoch != self._epoch:
             if self.exact:
                 host = torch.tensor(self._stream.epoch_list(epoch), dtype=torch.int64)

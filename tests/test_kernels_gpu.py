@@ -72,6 +72,21 @@ def test_batch_indexer_device_matches_host():
             assert ix(t).cpu().tolist() == g.indices(t), (n, W, r, t)
 
 
+def test_batch_indexer_exact_order_from_the_device_ring():
+    """The exact DistributedSampler order (module engine, split module path) gathered on
+    the device from the permutation ring equals torch's order, across epochs and with
+    the padded last positions of an uneven split."""
+    from distributed_training_pytorch_amd.data.sampler import BatchIndexer, EpochIndexStream
+
+    for n, W, r, B in [(512, 1, 0, 256), (1000, 3, 2, 100), (37, 4, 3, 5)]:
+        g = SamplerGeometry(n=n, world=W, rank=r, batch=B, seed=5)
+        ix = BatchIndexer(g, DEV, exact_torch=True)
+        assert ix._ring is not None
+        stream = EpochIndexStream(g)
+        for t in range(3 * g.steps_per_epoch + 2):
+            assert ix(t).cpu().tolist() == stream.indices(t), (n, W, r, t)
+
+
 def test_sampler_device_matches_python():
     lib = nat.require(DEV)
     for n, W, r, B in [(512, 1, 0, 256), (512, 8, 3, 256), (1000, 3, 2, 100), (4096, 8, 7, 256)]:
