@@ -36,6 +36,10 @@ constexpr int kAdamTab = 1024;
 
 constexpr int kWaves = kBlock / kWave;
 
+#ifndef DTP_XWAIT
+#define DTP_XWAIT 1  // 0 (A/B builds only): no exchange-wait diagnostic (bench exchange_wait_us_per_step)
+#endif
+
 // entries base + tid + j * kBlock (j < J) of the host's Adam table for a launch starting
 // at step t0: {lr / (1 - b1^t1), sqrt(1 - b2^t1)} with t1 = t0 + e + 1, clamped to the
 // table's saturated last row
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       // all-reduce (sum) this model's gradient + loss over every rank through
       // the peers' xGMI-mapped receive buffers, inside the step (xgmi_core.h)
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, &xwait);
+      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr);
     }
 
     // advance the sampler / loss-ring position and gather the next step's first
@@ -528,7 +532,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     }
     if (tid == 0) a.step[model] = t0 + a.n_steps;
     if (kXgmi && tid == 0) a.epoch[model] = xepoch;
-    if (kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
+    if (DTP_XWAIT && kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
     stamp_launch(21);
   }
 }
@@ -875,7 +879,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     float gloss = mean_loss;
     if constexpr (kXgmi) {
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, &xwait);
+      gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr);
     }
     const int lslot_now = lslot;
     roll(epoch, bi);
@@ -920,7 +924,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   }
   if (tid == 0) a.step[model] = t0 + a.n_steps;
   if (kXgmi && tid == 0) a.epoch[model] = xepoch;
-  if (kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
+  if (DTP_XWAIT && kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
 }
 
 // ------------------------------------------------------------------------------
