@@ -93,18 +93,18 @@ DTP_DEV void lane_pos(int p, int& pf, int& pb, int& tp) {
   static_for<0, NL>([&](auto LC) {
     constexpr int l = decltype(LC)::value;
     constexpr int I = S::din(l), O = S::dout(l);
-    constexpr int base = SC::tile(l) * 256, ro = SC::rowoff(l), co = SC::coloff(l);
+    constexpr int base = SC::tile(l) * SC::TSZ, ro = SC::rowoff(l), co = SC::coloff(l);
     if (p >= S::gw(l) && p < S::gb(l)) {
       const int q = p - S::gw(l), j = q / I, i = q - j * I;
       if constexpr (l < NL - 1) pf = C::f_off(l) + (i * L + j / NO) * NOP + j % NO;
       else pf = C::f_last() + j * C::RW + i;
       if constexpr (l >= 1) pb = C::b_off(l) + (j * L + i / NO) * NOP + i % NO;
-      tp = base + (ro + j) * 16 + co + i;
+      tp = base + SC::tslot(ro + j, co + i);
     } else if (p >= S::gb(l) && p < S::gb(l) + O) {
       const int j = p - S::gb(l);
       if constexpr (l < NL - 1) pf = C::f_off(l) + (I * L + j / NO) * NOP + j % NO;
       else pf = C::f_last() + j * C::RW + I;
-      tp = base + (ro + j) * 16 + co + I;  // bias column = constant-1 input
+      tp = base + SC::tslot(ro + j, co + I);  // bias column = constant-1 input
     }
   });
 }

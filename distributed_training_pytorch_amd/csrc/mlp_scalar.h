@@ -65,6 +65,12 @@ struct Scal {
   static constexpr int coloff(int l) { return (PACK && l == NL - 1) ? S::IN + 1 : 0; }
   static constexpr int lossrow() { return rowoff(NL - 1) + S::OUT; }
   static constexpr int losscol() { return coloff(NL - 1) + S::din(NL - 1); }  // last layer's bias column
+  // a parked dW tile (cross-wave reduction): column-major, column stride 20 floats, so a
+  // lane's 4 accumulator rows are one conflict-free ds_write_b128 (8 lanes of one column
+  // quarter hit 8 distinct 4-bank windows)
+  static constexpr int TSZ = 16 * 20;
+  static constexpr int tslot(int row, int col) { return col * 20 + row; }
+  static constexpr int losspos() { return tile(NL - 1) * TSZ + tslot(lossrow(), losscol()); }
   static_assert(S::OUT + 1 <= 16, "the loss row must fit under the output rows");
 };
 
@@ -80,18 +86,18 @@ DTP_DEV void scal_pos(int p, int& pf, int& pb, int& tpos, int& pfl) {
   static_for<0, S::NL>([&](auto LC) {
     constexpr int l = decltype(LC)::value;
     constexpr int I = S::din(l), O = S::dout(l);
-    constexpr int base = SC::tile(l) * 256, ro = SC::rowoff(l), co = SC::coloff(l);
+    constexpr int base = SC::tile(l) * SC::TSZ, ro = SC::rowoff(l), co = SC::coloff(l);
     if (p >= S::gw(l) && p < S::gb(l)) {
       const int q = p - S::gw(l), j = q / I, i = q - j * I;
       pf = SC::fwo(l) + i * SC::pad2(O) + j;
       if constexpr (l >= 1) pb = SC::lbo(l) + j * SC::pad4(I) + i;
       pfl = SC::lfo(l) + i * SC::pad4(O) + j;
-      tpos = base + (ro + j) * 16 + co + i;
+      tpos = base + SC::tslot(ro + j, co + i);
     } else if (p >= S::gb(l) && p < S::gb(l) + O) {
       const int j = p - S::gb(l);
       pf = SC::fbo(l) + j;
       pfl = SC::lfb(l) + j;
-      tpos = base + (ro + j) * 16 + co + I;  // bias column = constant-1 input
+      tpos = base + SC::tslot(ro + j, co + I);  // bias column = constant-1 input
     }
   });
 }

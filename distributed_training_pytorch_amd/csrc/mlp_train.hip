@@ -121,7 +121,7 @@ template <class S, int MODE, bool PROF = false, bool FAST = false>
 __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT;
-  static_assert(NT * 256 <= 2 * 2 * kStgArr, "a wave's reduction tiles must fit in its staging area");
+  static_assert(NT * SC::TSZ <= 2 * 2 * kStgArr, "a wave's reduction tiles must fit in its staging area");
   __shared__ __align__(16) TrainSmem<S> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
@@ -417,11 +417,8 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     {
       const int q = lane >> 4, col = lane & 15;
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        float* tl = &sm.stage[wave][0][0] + tt * 256;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tl[(4 * q + r) * 16 + col] = acc[tt][r];
-      }
+      for (int tt = 0; tt < NT; ++tt)
+        *reinterpret_cast<f32x4*>(&sm.stage[wave][0][0] + tt * SC::TSZ + SC::tslot(4 * q, col)) = acc[tt];
     }
     __syncthreads();
     // this step's Adam scalars: requested now, consumed after the reduction
@@ -432,16 +429,15 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     float g[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int tt = tp[k] >> 8, e = tp[k] & 255;
       float s = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) s += sm.stage[ww][0][tt * 256 + e];
+      for (int ww = 0; ww < kWaves; ++ww) s += sm.stage[ww][0][tp[k]];
       g[k] = s;
     }
     float lsum = 0.f;
 #pragma unroll
     for (int ww = 0; ww < kWaves; ++ww)
-      lsum += S::BF ? sm.lossw[ww] : sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+      lsum += S::BF ? sm.lossw[ww] : sm.stage[ww][0][SC::losspos()];
     const float mean_loss = lsum * inv;
     DTP_STAMP(5);
 
@@ -559,7 +555,7 @@ struct LaneSmem {
   using C = LaneCfg<S, L>;
   alignas(16) float wb[C::pad4(C::LW)];
   alignas(16) float stg[NW][lane_areas<S>()][2 * C::AREA];  // per wave, per area: dz operand, h operand
-  alignas(16) float red[NW][Scal<S>::NT * 256];             // per-wave partial dW tiles
+  alignas(16) float red[NW][Scal<S>::NT * Scal<S>::TSZ];             // per-wave partial dW tiles
   alignas(16) float2 adam_tab[kAdamTab];
   alignas(16) float data[kLaneData];
   float sink[4];
@@ -855,10 +851,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     {
       const int q = lane >> 4, col = lane & 15;
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sm.red[wave][tt * 256 + (4 * q + r) * 16 + col] = acc[tt][r];
-      }
+      for (int tt = 0; tt < NT; ++tt)
+        *reinterpret_cast<f32x4*>(&sm.red[wave][tt * SC::TSZ + SC::tslot(4 * q, col)]) = acc[tt];
     }
     __syncthreads();
     const float2 adam_sc = sm.adam_tab[it % kAdamTab];
@@ -873,7 +867,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     }
     float lsum = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+    for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::losspos()];
     const float mean_loss = lsum * inv;
     DTP_STAMP(5);
     float gloss = mean_loss;

@@ -387,7 +387,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NPT = S::NPT, NT = SC::NT;
   static_assert(NL >= 2, "one-layer stages run split_stage_body_v1");
-  static_assert(NT * 256 <= 2 * kStgArr, "a wave's reduction tiles fit its staging area");
+  static_assert(NT * SC::TSZ <= 2 * kStgArr, "a wave's reduction tiles fit its staging area");
   static_assert(sizeof(SplitPipeSmem<S>) <= kSplitSmemBytes, "stage LDS exceeds the shared block");
   SplitPipeSmem<S>& sm = *reinterpret_cast<SplitPipeSmem<S>*>(smem);
   const bool adam = a.optim == DTP_MODE_ADAM;
@@ -614,8 +614,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       const int q = lane >> 4, col = lane & 15;
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) stg_pack[tt * 256 + (4 * q + r) * 16 + col] = acc[tt][r];
+        *reinterpret_cast<f32x4*>(stg_pack + tt * SC::TSZ + SC::tslot(4 * q, col)) = acc[tt];
     }
     __syncthreads();
     SPLIT_STAMP(5);
@@ -632,7 +631,7 @@ DTP_DEV void split_stage_body_pipe(const DtpSplitStageArgs& a, unsigned char* sm
       float ls = 0.f;
 #pragma unroll
       for (int ww = 0; ww < kBlock / kWave; ++ww)
-        ls += sm.stage[ww][0][SC::tile(NL - 1) * 256 + SC::lossrow() * 16 + SC::losscol()];
+        ls += sm.stage[ww][0][SC::losspos()];
       loss = ls * inv;
     }
     SPLIT_STAMP(6);
