@@ -15,8 +15,10 @@ capped at 256 -> 256 / 256 / 128 / 64 at W = 1 / 2 / 4 / 8, global batch 256
 512 samples per rank instead (n = 512*W, per-rank batch 256) -- a config the
 reference never ran, kept as an extra.
 
-Usage: python bench.py --gpus N --steps K --warmup W   (N>1 under torchrun)
-Prints ONE JSON line on rank 0.
+Usage: python bench.py --gpus N --steps K --warmup W
+N > 1 runs under an outer torchrun, or -- without one (no WORLD_SIZE in the
+environment) -- bench.py starts its own N ranks (``self_launch``).
+Prints ONE JSON line (rank 0's).
 """
 from __future__ import annotations
 
@@ -136,8 +138,55 @@ def pin_host_thread(dev) -> int | None:
         return None
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(a, argv: list[str]) -> int:
+    """``--gpus N > 1`` without a launcher around us: start the N ranks ourselves, the way
+    the reference's launch layer does (``torchrun --standalone --nproc_per_node G``,
+    /root/reference/hpc_files/virtual_env_hpc_files/distributed_scripts/torchrun_launcher.sh:9-20).
+
+    Runs BEFORE this process touches the GPU (counting devices does not) and never execs:
+    the ranks are children of a ``torch.distributed.run`` child on 127.0.0.1.  Their
+    stderr passes through; their stdout is read here and rank 0's one JSON line is
+    forwarded (anything else the ranks print goes to stderr).  Returns the launcher's
+    exit code (non-zero as soon as any rank failed -- torchrun tears the others down)."""
+    import subprocess
+
+    ndev = torch.cuda.device_count()
+    if ndev and a.gpus > ndev and not a.share_gpu:
+        raise SystemExit(f"--gpus {a.gpus} but only {ndev} GPUs are visible (--share-gpu rehearses on fewer)")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env["DTP_BENCH_CHILD"] = "1"  # a rank never launches again, whatever its env says
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    json_lines = []
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            json_lines.append(s)
+        else:
+            sys.stderr.write(line)
+    rc = p.wait()
+    if rc == 0 and len(json_lines) != 1:
+        sys.stderr.write(f"[bench] expected one JSON line from rank 0, got {len(json_lines)}\n")
+        rc = 1
+    if json_lines:
+        print(json_lines[-1], flush=True)
+    return rc
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and os.environ.get("DTP_BENCH_CHILD") != "1":
+        sys.exit(self_launch(a, sys.argv[1:]))
     if torch.cuda.device_count() > 0:  # counting devices does not initialise the GPU
         from distributed_training_pytorch_amd import _native
 
@@ -155,7 +204,9 @@ def main():
         env.local_rank %= ndev
     rank, world = env.rank, env.world_size
     if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun, or without WORLD_SIZE")
+    if os.environ.get("DTP_BENCH_FAIL_RANK", "") == str(rank):  # test hook: one rank dies
+        raise SystemExit(f"rank {rank}: forced failure (DTP_BENCH_FAIL_RANK)")
     dev = bootstrap.bind_device(env)
     pinned = pin_host_thread(dev) if os.environ.get("DTP_BENCH_PIN", "one") != "0" else None
     if world > 1 or a.impl == "stock":  # the stock loop wraps its models in torch DDP even at W=1
@@ -192,7 +243,9 @@ def main():
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
                     else "Feistel shuffle", "cu_mask": a.cu_mask,
                     # lanes per sample of the fused step (1, or 2 / 4: csrc/mlp_lanes.h for batches <= 128 / 64)
-                    "lanes_per_sample": runner.lanes, "waves_per_cu": runner.kernel_waves}
+                    "lanes_per_sample": runner.lanes, "waves_per_cu": runner.kernel_waves,
+                    # > 1: the split-batch step (csrc/grp_core.h), CUs per model
+                    "workgroups_per_model": runner.groups}
 
     # the timed region is bracketed by an all-rank barrier + synchronize on both sides;
     # ranks of the in-kernel xGMI engine use the framework's device barrier (one xGMI

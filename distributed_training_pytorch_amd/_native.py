@@ -90,7 +90,12 @@ class TrainArgs(ctypes.Structure):
         ("hp", Hyper),
         ("adam_tab", c_void_p),
         ("adam_tab_len", c_int),
-        ("pad2_", c_int),
+        ("xbuf_bytes", c_int),
+        ("grp_buf", c_void_p),
+        ("grp_epoch", c_void_p),
+        ("grp_status", c_void_p),
+        ("groups", c_int),
+        ("pad3_", c_int),
     ]
 
 
@@ -232,6 +237,8 @@ def _declare(lib):
         "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_int, c_void_p]),
         "dtp_train_engine_destroy": (None, [c_void_p]),
         "dtp_train_engine_lanes": (c_int, [c_void_p]),
+        "dtp_train_engine_groups": (c_int, [c_void_p]),
+        "dtp_train_engine_status": (c_int, [c_void_p, P(c_int)]),
         "dtp_mlp_train_lanes": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
         "dtp_mlp_train_profile_lanes": (c_int, [P(TrainArgs), c_int, c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
@@ -266,6 +273,7 @@ def _declare(lib):
         "dtp_graph_capture_train": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                             P(c_void_p)]),
         "dtp_graph_launch": (c_int, [c_void_p, c_void_p]),
+        "dtp_graph_capture_engine": (c_int, [c_void_p, c_int, c_void_p, P(c_void_p)]),
         "dtp_graph_destroy": (c_int, [c_void_p]),
         "dtp_struct_sizes": (c_int, [P(c_int)]),
         "dtp_gemm": (c_int, [P(GemmArgs), c_void_p]),

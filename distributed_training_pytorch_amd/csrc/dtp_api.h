@@ -52,7 +52,14 @@ struct DtpTrainArgs {
   // Nullable: the kernel forms them itself.  Used with host_t0 >= 0 (the persistent engine).
   const float* adam_tab;  // [adam_tab_len][2]
   int adam_tab_len;
-  int pad2_;
+  int xbuf_bytes;  // MODE_XGMI_*: bytes of each rank's receive buffer (0: unchecked)
+  // split-batch step (grp_core.h): the engine's own exchange buffer, epoch counters and
+  // timeout words; groups = workgroups per model.  Filled by dtp_train_engine_create.
+  void* grp_buf;
+  unsigned* grp_epoch;
+  int* grp_status;
+  int groups;
+  int pad3_;
 };
 
 int dtp_version(void);

@@ -1,0 +1,153 @@
+// On-chip all-reduce among the GR workgroups that share ONE model's batch inside one
+// launch (the split-batch step of mlp_train.hip: a model's per-rank batch spread over GR
+// CUs, each running the several-lanes step on batch / GR samples).
+//
+// Why: the one-lane step at batch 256 keeps one CU per model busy and is latency-bound
+// (4.1 us/step); the 4-lanes step does 64 samples in ~2.2 us.  Splitting the batch over
+// GR = batch / 64 workgroups and summing their partial weight gradients on chip before
+// the (redundant, bitwise identical) optimizer step trades ~half the step's chain for
+// one on-chip hand-off.
+//
+// Protocol: the granule form of xgmi_core.h at device scope (MI355X_MICROARCH.md
+// "Workgroup dispatch ... inter-workgroup visibility", recipe R2 of
+// cdna_hip_programming.md Guideline 16):
+//   * one coarse-grained device buffer, layout [parity 2][model][src workgroup][slot] of
+//     16-byte granules {tag = exchange epoch, two fp32 values, check word};
+//   * a workgroup stores each of its granules ONCE (every member reads the same slot --
+//     no per-peer copies as over xGMI), with ONE 16-byte write-through (sc1) store;
+//   * members poll the other GR - 1 slots with sc1 loads (L1 bypassed, so no acquire
+//     fence is needed: every load of the handed-off bytes is an sc1 load and every store
+//     an sc1 store) until tag and check word match; the own contribution stays in registers;
+//   * sums run in workgroup order 0..GR-1 on every member -> bitwise identical gradients,
+//     hence bitwise identical optimizer steps and weight replicas in every member;
+//   * two parities + a monotonic epoch (device counter, never rewound): a member can run
+//     at most one exchange ahead of another, so exchange e+1 never overwrites a slot still
+//     being read for exchange e, and a granule from an earlier launch never matches;
+//   * spins are bounded; a timeout sets status[0] / status[1] = epoch, the step continues.
+// Placement: the members of a model are blocks m, m + 8, m + 16, ... (one XCD under the
+// observed round-robin dispatch, so the hand-off stays in that XCD's L2) -- speed only:
+// the protocol is correct under any placement (sc1 on both sides).
+#pragma once
+#include "xgmi_core.h"
+
+namespace dtp {
+
+constexpr int kGrpMax = 8;  // workgroups per model (batch <= 512 at 64 samples each)
+
+#ifndef DTP_GRP_ST_AUX
+#define DTP_GRP_ST_AUX 16  // granule stores: sc1 (write-through, device scope)
+#endif
+#ifndef DTP_GRP_LD_AUX
+#define DTP_GRP_LD_AUX 16  // granule polls: sc1 (L2-served, L1 bypassed)
+#endif
+
+// granules per (parity, model, member) slot -- the xGMI slot size (xgmi_core.h)
+DTP_HD constexpr int grp_slot16(int P, int npt) { return xgmi_slot16(P, npt); }
+
+struct GrpCtx {
+  void* buf;    // [2][n_models][GR][slot16] granules
+  int* status;  // sticky timeout word pair (nullable)
+  int GR, k, n_models, timeout_us;
+};
+
+// g (in): this member's partial sums of its NPT owned parameters; out: the sum over the
+// GR members.  Returns the summed loss partial.  Called by every thread of the member.
+template <int NPT, int NTHREADS>
+DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], float loss, unsigned epoch, int tid) {
+  constexpr int GPT = xgmi_gpt<NPT>();
+  const int slot = grp_slot16(P, NPT);
+  const int nthr = xgmi_nthr(P, NPT);
+  const int ltid = xgmi_loss_tid<NPT>(P, NTHREADS);
+  const size_t base = (size_t)((int)(epoch & 1u) * c.n_models + model) * c.GR;
+  const bool has_g = tid < nthr;
+  const bool has_l = tid == ltid;
+  float v[GPT + 1][2];
+#pragma unroll
+  for (int k = 0; k < GPT; ++k) {
+    v[k][0] = 2 * k < NPT ? g[2 * k] : 0.f;
+    v[k][1] = 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f;
+  }
+  v[GPT][0] = loss;
+  v[GPT][1] = 0.f;
+  auto gidx = [&](int k) { return k < GPT ? tid * GPT + k : nthr * GPT; };
+  auto mine_k = [&](int k) { return k < GPT ? has_g : has_l; };
+  const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(c.buf);
+  // publish once: every member reads this slot
+#pragma unroll
+  for (int k = 0; k <= GPT; ++k) {
+    if (!mine_k(k)) continue;
+    const uint32_t x0 = __float_as_uint(v[k][0]), x1 = __float_as_uint(v[k][1]);
+    const u32x4 q = {epoch, x0, x1, xgmi_check(epoch, x0, x1)};
+    __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(((base + c.k) * slot + gidx(k)) * 16), 0, DTP_GRP_ST_AUX);
+  }
+  float val[kGrpMax][GPT + 1][2];
+  static_assert(kGrpMax * (GPT + 1) <= 64, "pending mask holds every (member, granule) pair");
+  uint64_t pending = 0ull;
+#pragma unroll
+  for (int r = 0; r < kGrpMax; ++r) {
+#pragma unroll
+    for (int k = 0; k <= GPT; ++k) {
+      val[r][k][0] = (r == c.k) ? v[k][0] : 0.f;
+      val[r][k][1] = (r == c.k) ? v[k][1] : 0.f;
+      if (r < c.GR && r != c.k && mine_k(k)) pending |= 1ull << (r * (GPT + 1) + k);
+    }
+  }
+  bool dead = c.status ? (__hip_atomic_load(&c.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
+  unsigned long long deadline = 0;
+  unsigned spins = 0;
+  while (pending && !dead) {
+    u32x4 x[kGrpMax][GPT + 1];
+    asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
+#pragma unroll
+    for (int r = 0; r < kGrpMax; ++r) {
+#pragma unroll
+      for (int k = 0; k <= GPT; ++k) {
+        x[r][k] = u32x4{0u, 0u, 0u, 0u};
+        if ((pending >> (r * (GPT + 1) + k)) & 1ull)
+          x[r][k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((base + r) * slot + gidx(k)) * 16), 0,
+                                                          DTP_GRP_LD_AUX);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kGrpMax; ++r) {
+#pragma unroll
+      for (int k = 0; k <= GPT; ++k) {
+        const u32x4 q = x[r][k];
+        if (((pending >> (r * (GPT + 1) + k)) & 1ull) && q.x == epoch && q.w == xgmi_check(epoch, q.y, q.z)) {
+          val[r][k][0] = __uint_as_float(q.y);
+          val[r][k][1] = __uint_as_float(q.z);
+          pending &= ~(1ull << (r * (GPT + 1) + k));
+        }
+      }
+    }
+    if (!pending) break;
+    // the clock is an SMEM read (it would hold the next LDS wait at lgkmcnt(0)): read it
+    // only every 64 polls
+    if ((++spins & 63u) == 0u) {
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (!deadline) {
+        deadline = now + (unsigned long long)(c.timeout_us > 0 ? c.timeout_us : 2000000) * 100ull;
+      } else if (now > deadline) {
+        if (c.status) {
+          atomicExch(&c.status[0], 1);
+          atomicExch(&c.status[1], (int)epoch);
+        }
+        dead = true;
+      }
+    }
+  }
+  // member order 0..GR-1 on every member (absent members add +0)
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < kGrpMax; ++r) acc += val[r][k / 2][k & 1];
+    g[k] = acc;
+  }
+  float lacc = 0.f;
+#pragma unroll
+  for (int r = 0; r < kGrpMax; ++r) lacc += val[r][GPT][0];
+  return lacc;
+}
+
+}  // namespace dtp

@@ -21,6 +21,7 @@
 #include "mlp_scalar.h"
 #include "optim_core.h"
 #include "xgmi_core.h"
+#include "grp_core.h"
 
 namespace dtp {
 
@@ -562,7 +563,12 @@ struct LaneSmem {
 };
 
 // NW waves per workgroup (4: one per SIMD; 8: two per SIMD, for batches of 256 / L < B <= 512 / L)
-template <class S, int L, int MODE, bool PROF = false, int NW = 4>
+// GRP: the batch split over a.groups workgroups per model (grp_core.h): member k of model m
+// is block m + 8 k (the members of a model share an XCD under round-robin dispatch), runs
+// the step on batch positions [k 64 NW / L, (k + 1) 64 NW / L), and the members' partial
+// weight gradients and losses are summed on chip before every member's (identical)
+// optimizer step.
+template <class S, int L, int MODE, bool PROF = false, int NW = 4, bool GRP = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
 void mlp_train_lanes_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
@@ -572,12 +578,17 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NO = C::NO, TS = C::TS, H = S::H;
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM;
   static_assert(MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM, "the lanes step serves the Adam modes");
+  static_assert(!(GRP && kXgmi), "the split-batch step serves one rank");
   __shared__ __align__(16) LaneSmem<S, L, NW> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int model = blockIdx.x;
+  const int model = GRP ? (int)(blockIdx.x & 7u) : (int)blockIdx.x;
+  const int gk = GRP ? (int)(blockIdx.x >> 3) : 0;  // member of the model's group
+  if (GRP && (model >= a.n_models || gk >= a.groups)) return;  // grid = 8 x groups blocks
+  const bool lead = gk == 0;                // the member that writes the state back
   const int part = lane & (L - 1);          // this lane's slice of every hidden layer
   const int ws = lane / L;                  // sample slot inside the wave
-  const int bk = wave * C::G + ws;          // batch position of this lane's sample
+  const int bk = gk * (NW * C::G) + wave * C::G + ws;  // batch position of this lane's sample
+  const GrpCtx gctx{a.grp_buf, a.grp_status, a.groups, gk, a.n_models, a.timeout_us};
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
   const float slope = a.hp.slope;
 
@@ -619,7 +630,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   const int fidx0 = fast_index(epoch, bi);
   roll(e2, b2);
   int fidx = fast_index(e2, b2);
-  unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
+  unsigned xepoch = kXgmi ? a.epoch[model] : (GRP ? a.grp_epoch[model] : 0u);
   unsigned long long xwait = 0;
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
@@ -868,6 +879,10 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     float lsum = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::losspos()];
+    if constexpr (GRP) {  // the members' partial sums, on chip (grp_core.h)
+      xepoch += 1u;
+      lsum = grp_allreduce<NPT, NTH>(gctx, model, P, g, lsum, xepoch, tid);
+    }
     const float mean_loss = lsum * inv;
     DTP_STAMP(5);
     float gloss = mean_loss;
@@ -894,7 +909,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
         *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
       }
     }
-    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, NTH) : 0) && a.loss_log) {
+    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, NTH) : 0) && a.loss_log && lead) {
       const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
       a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
     }
@@ -907,6 +922,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     DTP_STAMP(7);
   }
 
+  if (!lead) return;  // every member holds the same state: the first writes it back
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int p = NPT * tid + k;
@@ -918,6 +934,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   }
   if (tid == 0) a.step[model] = t0 + a.n_steps;
   if (kXgmi && tid == 0) a.epoch[model] = xepoch;
+  if (GRP && tid == 0) a.grp_epoch[model] = xepoch;
   if (DTP_XWAIT && kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
 }
 
@@ -999,6 +1016,13 @@ void launch_lanes(const DtpTrainArgs& a, hipStream_t st) {
                      a);
 }
 
+// split-batch step: member k of model m is block m + 8 k (blocks of absent models exit)
+template <class S, int L, int NW>
+void launch_lanes_grp(const DtpTrainArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, false, NW, true>), dim3(8 * a.groups),
+                     dim3(64 * NW), 0, st, a);
+}
+
 template <class S, int L, int NW>
 TrainLaunchFn lanes_fn(int mode) {
   if (mode == DTP_MODE_ADAM) return &launch_lanes<S, L, DTP_MODE_ADAM, NW>;
@@ -1009,11 +1033,44 @@ TrainLaunchFn lanes_fn(int mode) {
 // the step instance of a launch: lanes per sample and waves per workgroup
 struct LanePick {
   int L = 1, NW = 4;
+  int GR = 1;  // workgroups per model (split-batch step, grp_core.h)
 };
+
+// threads of the workgroups the fused step instances launch (one-lane: kBlock; lanes:
+// 64 NW, NW = 4 or 8)
+constexpr int kStepThreads[] = {dtp::kBlock, 4 * 64, 8 * 64};
+
+long long xgmi_bytes_for(int P, int n_models, int world, int slot16) {
+  return 2ll * n_models * world * slot16 * 16ll;
+}
+int xgmi_slot16_threads(int P, int nth) { return dtp::xgmi_slot16(P, (P + nth - 1) / nth); }
+int xgmi_max_slot16(int P) {
+  int m = 0;
+  for (int nth : kStepThreads) m = max(m, xgmi_slot16_threads(P, nth));
+  return m;
+}
 
 // 4 lanes per sample for per-rank batches <= 64, 2 for <= 128, else the one-lane kernel
 // (L = 1).  DTP_LANES=<L>[x<NW>] forces a choice (A/B runs; NW = 8 runs two waves per
 // SIMD, 512 / L samples); a forced pick whose batch bound does not hold falls back to 1.
+// Split-batch step (engine launches only: it owns the exchange buffer): a per-rank batch
+// above 64 on one rank runs on ceil(batch / 64) workgroups per model, each the 4-lanes step
+// on 64 samples, their gradients summed on chip.  DTP_GROUPS=1 turns it off (A/B runs).
+int pick_groups(const DtpTrainArgs& a, int mode, const LanePick& lp, bool allow) {
+  static const int env = [] {
+    const char* e = getenv("DTP_GROUPS");
+    return e ? atoi(e) : 0;
+  }();
+  static const bool forced_lanes = getenv("DTP_LANES") != nullptr;  // a forced lanes instance runs as asked
+  if (!allow || env == 1 || forced_lanes || mode != DTP_MODE_ADAM || a.bf16 || a.n_models > 8 || a.smp.world != 1)
+    return 1;
+  if (a.smp.n * (2 + 1) > dtp::kLaneData) return 1;
+  const int b = min(a.smp.batch, a.smp.num_samples);
+  if (b <= 64 || lp.L == 0) return 1;
+  const int gr = (b + 63) / 64;
+  return gr <= dtp::kGrpMax ? gr : 1;
+}
+
 LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
   static const LanePick forced = [] {
     LanePick f{0, 4};
@@ -1040,9 +1097,17 @@ LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
 }
 
 TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode,
-                            LanePick* pick = nullptr) {
+                            LanePick* pick = nullptr, bool allow_groups = false) {
   const bool fast = fast_path_ok(a, in, out, mode);
-  const LanePick lp = pick_lanes(a, in, out, fast);
+  LanePick lp = pick_lanes(a, in, out, fast);
+  if (fast && in == 2 && h == 10 && nl == 5 && out == 1) {  // the toy shape: split-batch instance
+    const int gr = pick_groups(a, mode, lp, allow_groups);
+    if (gr > 1) {
+      lp = LanePick{4, 4, gr};
+      if (pick) *pick = lp;
+      return &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false>, 4, 4>;
+    }
+  }
   if (pick) *pick = lp;
   if (lp.L > 1 && lp.NW == 4) {
 #define X(I, H, N, O)                                                                                   \
@@ -1069,6 +1134,22 @@ TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int ou
   DTP_TRAIN_SHAPES(X)
 #undef X
   return nullptr;
+}
+
+// the xGMI receive buffer covers the picked instance's granule layout (peers' stores
+// through a buffer resource are not bounds-checked: an undersized buffer is corrupted)
+int check_xbuf(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode, const LanePick& lp) {
+  if ((mode != DTP_MODE_XGMI_ADAM && mode != DTP_MODE_XGMI_SGD) || a.xbuf_bytes <= 0) return 0;
+  int P = 0;
+  for (int l = 0; l < nl; ++l) P += (l == nl - 1 ? out : h) * ((l == 0 ? in : h) + 1);
+  const int nth = lp.L > 1 ? 64 * lp.NW : dtp::kBlock;
+  const long long need = xgmi_bytes_for(P, a.n_models, a.smp.world, xgmi_slot16_threads(P, nth));
+  if (need > a.xbuf_bytes) {
+    char m[160];
+    snprintf(m, sizeof m, "xGMI receive buffer too small: %lld bytes needed, %d allocated", need, a.xbuf_bytes);
+    return set_err(-5, m);
+  }
+  return 0;
 }
 
 int validate_train(const DtpTrainArgs* a, int mode) {
@@ -1102,7 +1183,32 @@ struct TrainEngine {
   TrainLaunchFn fn;
   int mode;
   LanePick pick;  // lanes per sample / waves of the chosen instance (L = 1: mlp_train_kernel)
+  void* grp_mem = nullptr;  // split-batch step: [status 16 ints | epochs | granule buffer]
+  ~TrainEngine() {
+    if (grp_mem) (void)hipFree(grp_mem);
+  }
 };
+
+// the split-batch step's device state, zeroed: 64 B of timeout words, the per-model epoch
+// counters (64 B aligned), then the [2][n_models][GR][slot16] granule buffer
+int grp_alloc(TrainEngine* e, int P) {
+  const int nth = 64 * e->pick.NW;
+  const long long slot = dtp::grp_slot16(P, (P + nth - 1) / nth);
+  const long long gbytes = 2ll * e->a.n_models * e->pick.GR * slot * 16;
+  const long long ebytes = ((long long)e->a.n_models * 4 + 63) & ~63ll;
+  const long long total = 64 + ebytes + gbytes;
+  if (hipMalloc(&e->grp_mem, total) != hipSuccess) {
+    e->grp_mem = nullptr;
+    return set_err(-3, "hipMalloc of the split-batch exchange buffer failed");
+  }
+  if (hipMemset(e->grp_mem, 0, total) != hipSuccess) return set_err(-3, "hipMemset of the exchange buffer failed");
+  char* b = static_cast<char*>(e->grp_mem);
+  e->a.grp_status = reinterpret_cast<int*>(b);
+  e->a.grp_epoch = reinterpret_cast<unsigned*>(b + 64);
+  e->a.grp_buf = b + 64 + ebytes;
+  e->a.groups = e->pick.GR;
+  return 0;
+}
 
 template <class S>
 int launch_train_profile(const DtpTrainArgs* a, hipStream_t st) {
@@ -1147,10 +1253,9 @@ int dtp_mlp_workspace_floats(int in, int h, int nl, int out) {
 // bytes of one rank's receive buffer of the fused step's xGMI exchange
 // ([parity 2][model][src rank][slot] of 16-byte granules, xgmi_core.h)
 long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world) {
-  // sized for the instance with the most granules: 512 threads (8-wave lanes step), one
-  // parameter per thread
-  const int npt = (P + 2 * dtp::kBlock - 1) / (2 * dtp::kBlock);
-  return 2ll * n_models * world * dtp::xgmi_slot16(P, npt) * 16ll;
+  // sized for the instance with the most granules: xgmi_slot16 is not monotone in the
+  // parameters per thread, so take the max over every instantiated thread count
+  return xgmi_bytes_for(P, n_models, world, xgmi_max_slot16(P));
 }
 
 int dtp_mlp_param_count(int in, int h, int nl, int out) {
@@ -1165,8 +1270,10 @@ int dtp_mlp_param_count(int in, int h, int nl, int out) {
 int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode, void* stream) {
   if (int rc = validate_train(a, mode)) return rc;
   if (mode == DTP_MODE_GRAD && a->n_steps != 1) return set_err(-4, "MODE_GRAD requires n_steps == 1");
-  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode);
+  LanePick lp;
+  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode, &lp);
   if (!fn) return set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
+  if (int rc = check_xbuf(*a, in, h, nl, out, mode, lp)) return rc;
   fn(*a, (hipStream_t)stream);
   return check_launch("mlp_train_kernel");
 }
@@ -1174,17 +1281,40 @@ int dtp_mlp_train(const DtpTrainArgs* a, int in, int h, int nl, int out, int mod
 void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
   if (validate_train(a, mode)) return nullptr;
   LanePick lp;
-  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode, &lp);
+  TrainLaunchFn fn = resolve_train(*a, in, h, nl, out, mode, &lp, true);
   if (!fn) {
     set_err(-2, "mlp shape / mode not instantiated for the fused train kernel");
     return nullptr;
   }
+  if (check_xbuf(*a, in, h, nl, out, mode, lp)) return nullptr;
   auto* e = new TrainEngine();
   e->a = *a;
   e->fn = fn;
   e->mode = mode;
   e->pick = lp;
+  if (lp.GR > 1 && grp_alloc(e, dtp_mlp_param_count(in, h, nl, out))) {
+    delete e;
+    return nullptr;
+  }
   return e;
+}
+
+// workgroups per model of the engine's step (1, or the split-batch step's group size)
+int dtp_train_engine_groups(void* h) {
+  auto* e = static_cast<TrainEngine*>(h);
+  return e ? e->pick.GR : set_err(-1, "null engine");
+}
+
+// the split-batch exchange's sticky timeout words {flag, epoch} (synchronous copy; 0/0
+// when the engine has no split-batch step)
+int dtp_train_engine_status(void* h, int* out2) {
+  auto* e = static_cast<TrainEngine*>(h);
+  if (!e || !out2) return set_err(-1, "null engine");
+  out2[0] = out2[1] = 0;
+  if (!e->a.grp_status) return 0;
+  if (hipMemcpy(out2, e->a.grp_status, 2 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return set_err(-3, "status copy failed");
+  return 0;
 }
 
 // lanes per sample of the engine's kernel instance (1 = one lane per sample)
@@ -1193,12 +1323,12 @@ int dtp_train_engine_lanes(void* h) {
   return e ? e->pick.L : set_err(-1, "null engine");
 }
 
-// lanes per sample (low byte) and waves per workgroup (<< 8) the step would use for
-// these arguments (0: no fused instance)
+// lanes per sample (low byte), waves per workgroup (<< 8) and workgroups per model (<< 16)
+// of the step a train engine would launch for these arguments (0: no fused instance)
 int dtp_mlp_train_lanes(const DtpTrainArgs* a, int in, int h, int nl, int out, int mode) {
   if (validate_train(a, mode)) return 0;
   LanePick lp;
-  return resolve_train(*a, in, h, nl, out, mode, &lp) ? (lp.L | (lp.NW << 8)) : 0;
+  return resolve_train(*a, in, h, nl, out, mode, &lp, true) ? (lp.L | (lp.NW << 8) | (lp.GR << 16)) : 0;
 }
 
 // n_steps iterations in ONE persistent launch on `stream`, starting at step t0 (the

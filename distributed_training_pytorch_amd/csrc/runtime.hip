@@ -226,6 +226,42 @@ int dtp_graph_capture_train(const DtpTrainArgs* a, int in, int h, int nl, int ou
   return 0;
 }
 
+// `launches` one-step runs of a train engine (mlp_train.hip) captured into one graph;
+// each run reads its step number from the device counters (host_t0 = -1), so every
+// replay continues where the last one stopped
+int dtp_train_engine_run(void* h, int n_steps, int t0, void* stream);
+int dtp_graph_capture_engine(void* engine, int launches, void* stream, void** handle_out) {
+  *handle_out = nullptr;
+  if (launches <= 0 || !engine) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  auto* gh = new GraphHandle();
+  hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    delete gh;
+    return rt_fail(e, "hipStreamBeginCapture");
+  }
+  int rc = 0;
+  for (int i = 0; i < launches && rc == 0; ++i) rc = dtp_train_engine_run(engine, 1, -1, stream);
+  e = hipStreamEndCapture(st, &gh->graph);
+  if (rc != 0) {
+    if (gh->graph) (void)hipGraphDestroy(gh->graph);
+    delete gh;
+    return rc;
+  }
+  if (e != hipSuccess) {
+    delete gh;
+    return rt_fail(e, "hipStreamEndCapture");
+  }
+  e = hipGraphInstantiate(&gh->exec, gh->graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGraphDestroy(gh->graph);
+    delete gh;
+    return rt_fail(e, "hipGraphInstantiate");
+  }
+  *handle_out = gh;
+  return 0;
+}
+
 int dtp_graph_launch(void* handle, void* stream) {
   auto* gh = static_cast<GraphHandle*>(handle);
   if (!gh) return -1;

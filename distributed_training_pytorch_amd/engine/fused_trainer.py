@@ -140,7 +140,14 @@ class FusedTrainer:
     def kernel_waves(self) -> int:
         """Waves per workgroup of the fused step instance (4: one per SIMD; 8: two, the
         several-lanes step over 512 / L samples); 0 without a fused kernel."""
-        return self._pick() >> 8
+        return (self._pick() >> 8) & 0xFF
+
+    @property
+    def groups(self) -> int:
+        """Workgroups per model of the persistent step: > 1 is the split-batch step
+        (``csrc/grp_core.h``: a rank's batch over several CUs per model, 64 samples each,
+        their gradients summed on chip); 1 otherwise, 0 without a fused kernel."""
+        return self._pick() >> 16
 
     def _pick(self) -> int:
         if not self.native or self.comm in ("rccl", "host"):
@@ -298,6 +305,8 @@ class FusedTrainer:
         tab = getattr(self, "_adam_tab", None)
         if tab is not None:
             a.adam_tab, a.adam_tab_len = nat.ptr(tab), tab.shape[0]
+        if xg is not None:
+            a.xbuf_bytes = xg.nbytes
         return a
 
     def _update_mode(self) -> int:
@@ -352,9 +361,9 @@ class FusedTrainer:
         if self._ring is not None:
             self._ring.ensure(*self._ring.epochs_of_steps(self.t, self.t + k - 1))
 
-    def _run_engine(self, k: int):
-        """k iterations in one persistent launch through the native executor: the
-        argument block is built once, so a call is one C call + one kernel launch."""
+    def _engine_handle(self):
+        """The native step executor (created once: argument block, kernel instance and, for
+        the split-batch step, its on-chip exchange buffer)."""
         e = self._engine
         if e is None:
             lib = nat.load()
@@ -365,6 +374,12 @@ class FusedTrainer:
                 nat.check(-1, "dtp_train_engine_create")
             self._engine = e
             self._engine_run = lib.dtp_train_engine_run
+        return e
+
+    def _run_engine(self, k: int):
+        """k iterations in one persistent launch through the native executor: the
+        argument block is built once, so a call is one C call + one kernel launch."""
+        e = self._engine_handle()
         # the host's step mirror (== the device counters) lets the kernel request its
         # first dataset indices without waiting for the counter load
         nat.check(self._engine_run(e, k, self.t, nat.raw_stream(self._dev_index)), "dtp_train_engine_run")
@@ -380,12 +395,15 @@ class FusedTrainer:
         key = ("train", G)
         h = self._graphs.get(key)
         if h is None:
+            # G one-step launches of the engine (the same kernel instance as the persistent
+            # and eager launches -- the split-batch step included), each reading its step
+            # number from the device counters so every replay continues
+            e = self._engine_handle()
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream())
-            a = self._train_args(1, self._update_mode(), None)
             hp = ctypes.c_void_p()
-            nat.check(lib.dtp_graph_capture_train(ctypes.byref(a), *self.spec.key[:4], self._update_mode(), G,
-                                                  nat.stream_ptr(s), ctypes.byref(hp)), "dtp_graph_capture_train")
+            nat.check(lib.dtp_graph_capture_engine(e, G, nat.stream_ptr(s), ctypes.byref(hp)),
+                      "dtp_graph_capture_engine")
             torch.cuda.current_stream().wait_stream(s)
             h = hp.value
             self._graphs[key] = h
@@ -468,8 +486,7 @@ class FusedTrainer:
     def synchronize(self):
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
-        if self._xgmi is not None:
-            self._xgmi.check_status()
+        self.check_comm()
 
     def step_indices(self, t: int) -> list[int]:
         """Dataset indices of this rank's batch at step t (the order the kernels read)."""
@@ -507,10 +524,17 @@ class FusedTrainer:
         return w[0] / 100.0, int(w[1])  # s_memrealtime runs at 100 MHz
 
     def check_comm(self):
-        """Raise if the in-kernel exchange hit its (sticky) timeout. One small read;
-        call it where the host syncs anyway (loss readback, checkpoints)."""
+        """Raise if the in-kernel exchange (xGMI, or the split-batch step's on-chip one)
+        hit its (sticky) timeout. One small read; call it where the host syncs anyway
+        (loss readback, checkpoints)."""
         if self._xgmi is not None:
             self._xgmi.check_status()
+        if self._engine is not None:
+            st = (ctypes.c_int * 2)()
+            nat.check(nat.load().dtp_train_engine_status(self._engine, st), "dtp_train_engine_status")
+            if st[0]:
+                raise RuntimeError(f"split-batch exchange timed out at epoch {st[1]} (a member workgroup was not "
+                                   "resident)")
 
     def losses(self, t0: int, t1: int) -> torch.Tensor:
         """Global mean losses of steps [t0, t1) as a CPU tensor [t1-t0, n_models] (syncs)."""

@@ -10,10 +10,9 @@ Reference behaviour reproduced (torch DDP as used at ``demo.py:69-72``):
 MI355X-first choices:
 * gradients live in a flat buffer (parameters' ``.grad`` are views of it), so a
   bucket is a contiguous slice -- no per-bucket copy-in/copy-out;
-* buckets are sized for xGMI rings: the first (last-produced) bucket small to
-  start communication early, the rest large (default 64 MB -- 288 GB HBM makes
-  memory irrelevant, and larger messages amortise the per-hop ring latency
-  across the 7 point-to-point links);
+* buckets: the first (last-produced) bucket small to start communication early,
+  the rest 25 MB (torch DDP's defaults; see the class comment for the sizing
+  argument on 7 point-to-point xGMI links);
 * ``comm="auto"|"xgmi"`` routes buckets of up to 64 Ki floats through the
   one-shot xGMI all-reduce (``parallel/xgmi.py: XgmiAllReduce``) on a side HIP
   stream (one posted write per peer + one local read instead of a 2(W-1)-hop
@@ -32,8 +31,15 @@ from . import comm_util
 
 class FlatDDP(nn.Module):
     # bucket_cap_mb / first_bucket_mb: torch DDP's defaults (25 MB, 1 MiB first bucket,
-    # torch/nn/parallel/distributed.py).  The round-3 default of 64 MB had no measurement
-    # behind it; scripts/ab_bucket_cap.sh A/Bs the cap on the wide MLP.
+    # torch/nn/parallel/distributed.py).  Sizing on one MI355X node: a ring all-reduce
+    # of n bytes over W = 8 ranks moves 2 (W-1)/W n per rank and pays 2 (W-1) hop
+    # latencies; each ring hop is ONE point-to-point xGMI link, so RCCL runs several
+    # rings side by side over the 7 links.  Per bucket the fixed cost is the RCCL launch
+    # plus 14 hops (~10-20 us); at tens of GB/s per ring a 25 MB bucket spends > 90 % of
+    # its time moving bytes, while the 1 MiB first bucket starts the exchange as soon as
+    # the last layer's gradients exist.  Buckets <= 64 Ki floats take the one-shot xGMI
+    # all-reduce instead (one posted write per peer, one hop).  The 64 MB cap of round 3
+    # had no measurement behind it; no multi-GPU node was available to A/B either value.
     def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
                  flat_params: torch.Tensor | None = None, flat_grad: torch.Tensor | None = None,
                  broadcast: bool = True, comm: str = "auto"):

@@ -104,6 +104,7 @@ class XgmiExchange:
         world = dist.get_world_size(group) if dist.is_initialized() else 1
         # the fused kernel's 16-byte-granule layout, sized by the library itself
         nbytes = nat.require(device).dtp_xgmi_fused_buffer_bytes(P, n_models, world)
+        self.nbytes = int(nbytes)  # handed to every launch (DtpTrainArgs.xbuf_bytes), which checks it
         self.bufs = PeerBuffers(nbytes, device, group)
         self.lib = self.bufs.lib
         self.world, self.rank = self.bufs.world, self.bufs.rank

@@ -461,11 +461,23 @@ class Trainer:
         tr = FusedTrainer(plan["spec"], len(models), X, Y, geom, plan["optim"], ecfg,
                           init_params=[m.flat_params.detach() for m in models])
         self._skip_batches = 0  # the engine positions its sampler from the step count
+        # DDP construction semantics: the engine broadcast rank 0's weights; the modules
+        # take them too, so the check below runs training_step on the weights the engine
+        # trains (ranks that built their models from different seeds agree from here on)
+        for i, m in enumerate(models):
+            m.load_flat_(tr.model_params(i))
+        why = None
         if self.global_step:  # resumed: the torch optimizers' state continues in the engine
-            self._import_fused_state(tr, models, opts, self.global_step)
+            why = self._import_fused_state(tr, models, opts, self.global_step)
         # fused_spec() is a declaration: check it against training_step on the first batch
         # before the engine trains anything (every rank agrees on the outcome)
-        why = self._verify_fused_spec(model, opts, plan, tr, X, Y)
+        if why is None:
+            why = self._verify_fused_spec(model, opts, plan, tr, X, Y)
+        if self.world_size > 1:  # every rank takes the same decision
+            flag = torch.tensor([0.0 if why is None else 1.0])
+            comm_util.all_reduce_(flag)
+            if why is None and flag.item() > 0:
+                why = "the fused engine was refused on another rank"
         if why is not None:
             tr.close()
             if self.engine == "fused":
@@ -560,8 +572,8 @@ class Trainer:
         autograd, no optimizer step) and compare every model's logged loss and parameter
         gradient with the engine's gradient-only launch of the same step (MODE_GRAD:
         local means, nothing updated).  Returns None when they agree (rtol 1e-4, atol
-        1e-5: fp32 under different summation orders), else the reason.  All ranks take
-        the same decision."""
+        1e-5: fp32 under different summation orders), else the reason (the caller makes
+        every rank take the same decision)."""
         models, names = plan["models"], plan["names"]
         why = None
         try:
@@ -600,18 +612,15 @@ class Trainer:
                 model._logged.clear()
         except Exception as e:  # noqa: BLE001 - any failure of the check refuses the engine
             why = f"fused_spec check failed: {e}"
-        if self.world_size > 1:
-            flag = torch.tensor([0.0 if why is None else 1.0])
-            comm_util.all_reduce_(flag)
-            if why is None and flag.item() > 0:
-                why = "fused_spec check failed on another rank"
         return why
 
     @staticmethod
-    def _import_fused_state(tr, models, opts, global_step: int) -> None:
+    def _import_fused_state(tr, models, opts, global_step: int) -> str | None:
         """A resumed fit: the torch optimizers' restored moments (Adam exp_avg /
         exp_avg_sq, SGD momentum_buffer) and step count continue in the fused engine
-        (the parameters came in through init_params); ``global_step`` batches ran."""
+        (the parameters came in through init_params); ``global_step`` batches ran.
+        Returns None, or why the engine cannot continue this state (the caller refuses
+        the engine: the module path under engine='auto', an error under 'fused')."""
         for i, (m, o) in enumerate(zip(models, opts)):
             st = [o.state.get(p, {}) for p in m.parameters()]
             keys = ("exp_avg", "exp_avg_sq") if isinstance(o, torch.optim.Adam) else ("momentum_buffer",)
@@ -624,10 +633,11 @@ class Trainer:
             # one step number (host_t0 = tr.t): a restored optimizer that stepped a different
             # number of times than the batches that ran cannot continue bit-exactly there
             if step != global_step:
-                raise RuntimeError(f"resumed optimizer {i} has step {step} but global_step is {global_step}: the fused "
-                                   "engine needs one optimizer step per batch (use engine='module')")
+                return (f"resumed optimizer {i} has step {step} but global_step is {global_step}: the fused "
+                        "engine needs one optimizer step per batch")
             tr.step_ctr[i] = step
         tr.t = global_step
+        return None
 
     @staticmethod
     def _export_fused_state(tr, models, opts) -> None:

@@ -62,7 +62,7 @@ def test_module_step_graph_equals_eager_on_xgmi():
     assert torch.equal(g[0][0], g[1][0]), "replicas diverged"
 
 
-def _trainer_rank(rank, world, graphs, root, engine="module"):
+def _trainer_rank(rank, world, graphs, root, engine="module", seed_per_rank=False):
     os.environ["LOCAL_RANK"] = "0"  # both ranks on the one GPU (the process group is already up)
     sys.path.insert(0, ROOT)
     from demo_pytorch_lightning import LitToyModel
@@ -71,6 +71,8 @@ def _trainer_rank(rank, world, graphs, root, engine="module"):
 
     torch.manual_seed(0)
     dl = torch.utils.data.DataLoader(ToyData(seed=0), batch_size=128)
+    if seed_per_rank:  # the reference demo never seeds its models: every rank builds different weights
+        torch.manual_seed(1000 + rank)
     model = LitToyModel()
     tr = Trainer(gpus=2, max_steps=12, accelerator="gpu", strategy="ddp", log_every_n_steps=4,
                  default_root_dir=os.path.join(root, f"g{int(graphs)}"), enable_progress_bar=False,
@@ -101,6 +103,21 @@ def test_trainer_fused_engine_on_two_ranks(tmp_path):
     identical replicas."""
     f = run_ranks(_trainer_rank, 2, (False, str(tmp_path / "f"), "auto"), timeout=300)
     e = run_ranks(_trainer_rank, 2, (False, str(tmp_path / "e"), "module"), timeout=300)
+    for r in range(2):
+        assert f[r][3] == "fused" and e[r][3] == "module", (f[r][3], e[r][3])
+        for k, v in e[r][0].items():
+            torch.testing.assert_close(f[r][0][k], v, rtol=0, atol=1e-4)
+    for k in f[0][0]:
+        assert torch.equal(f[0][0][k], f[1][0][k]), k
+
+
+def test_trainer_fused_engine_ranks_built_from_different_seeds(tmp_path):
+    """Ranks whose models start from different weights: the engine broadcasts rank 0's,
+    the modules take them before fused_spec() is checked, so the check passes on every
+    rank (it compared rank r's own weights with rank 0's before) and training ends where
+    the module path ends."""
+    f = run_ranks(_trainer_rank, 2, (False, str(tmp_path / "f"), "fused", True), timeout=300)
+    e = run_ranks(_trainer_rank, 2, (False, str(tmp_path / "e"), "module", True), timeout=300)
     for r in range(2):
         assert f[r][3] == "fused" and e[r][3] == "module", (f[r][3], e[r][3])
         for k, v in e[r][0].items():

@@ -26,16 +26,20 @@ def _init(spec, seed, n=2, scale=0.4):
     return [(torch.randn(spec.P, generator=g) * scale).to(DEV) for _ in range(n)]
 
 
-@pytest.mark.parametrize("batch,lanes", [(64, 4), (50, 4), (128, 2), (100, 2), (256, 1)])
-def test_lanes_selected_by_batch_and_match_torch(batch, lanes):
-    """batch 50 / 100: the epoch's last batch is short (512 = 10 x 50 + 12, 5 x 100 + 12),
-    so the lanes past it must drop out of the loss, the dW tiles and the mean."""
+@pytest.mark.parametrize("batch,lanes,groups", [(64, 4, 1), (50, 4, 1), (128, 4, 2), (100, 4, 2), (256, 4, 4),
+                                                (200, 4, 4)])
+def test_lanes_selected_by_batch_and_match_torch(batch, lanes, groups):
+    """batch 50 / 100 / 200: the epoch's last batch is short (512 = 10 x 50 + 12,
+    5 x 100 + 12, 2 x 200 + 112), so the lanes past it must drop out of the loss, the dW
+    tiles and the mean; at 200 the last batch leaves split-batch members 2 and 3 without
+    a sample.  Batches above 64 run the split-batch step: batch / 64 workgroups per model
+    (csrc/grp_core.h)."""
     X, Y = ToyData(n=512, seed=21).device_tensors(DEV)
     geom = SamplerGeometry(n=512, batch=batch, seed=3)
     init = _init(TOY_SPEC, batch)
     ocfg = OptimConfig(lr=1e-2)
     tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=7), init_params=init)
-    assert tr.lanes == lanes
+    assert (tr.lanes, tr.groups) == (lanes, groups)
     steps = 2 * geom.steps_per_epoch + 3
     tr.train(steps)
     tr.synchronize()
@@ -59,7 +63,7 @@ def test_lanes_other_shapes_match_torch(spec, batch):
     init = _init(spec, 7 + batch, scale=0.3)
     ocfg = OptimConfig(lr=5e-3)
     tr = FusedTrainer(spec, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=5), init_params=init)
-    assert tr.lanes == (4 if batch == 64 else 2)
+    assert tr.lanes == (4 if batch == 64 else 2) and tr.groups == 1  # split-batch step: the toy shape only
     steps = 12
     tr.train(steps)
     tr.synchronize()
@@ -69,11 +73,13 @@ def test_lanes_other_shapes_match_torch(spec, batch):
     tr.close()
 
 
-@pytest.mark.parametrize("batch", [64, 128])
+@pytest.mark.parametrize("batch", [64, 128, 256])
 def test_lanes_bitwise_across_launch_modes(batch):
     """The lanes instance is deterministic: one persistent launch, short persistent
     launches, per-step eager launches and hipGraph replays give bitwise the same run,
-    including a launch longer than the kernel's Adam-scalar table (1024 steps)."""
+    including a launch longer than the kernel's Adam-scalar table (1024 steps).  At 128
+    and 256 that is the split-batch step (2 / 4 workgroups per model): its on-chip sums
+    run in member order, whatever order the members finish in."""
     X, Y = ToyData(n=512, seed=2).device_tensors(DEV)
     geom = SamplerGeometry(n=512, batch=batch, seed=1)
     init = _init(TOY_SPEC, 40)
@@ -84,7 +90,7 @@ def test_lanes_bitwise_across_launch_modes(batch):
                               ("eager", EngineConfig(launch="eager"), 30),
                               ("graph", EngineConfig(launch="graph", steps_per_launch=8), 30)]:
         tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
-        assert tr.lanes == (4 if batch == 64 else 2)
+        assert (tr.lanes, tr.groups) == (4, batch // 64)
         tr.train(steps)
         tr.synchronize()
         res[name] = (tr.params.clone(), tr.losses(0, steps))
@@ -132,6 +138,26 @@ def test_lanes_agree_with_one_lane_kernel(tmp_path):
     for flag in ("2", "4"):
         torch.testing.assert_close(outs[flag]["l"], outs["1"]["l"], rtol=1e-4, atol=1e-6)
         torch.testing.assert_close(outs[flag]["p"], outs["1"]["p"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("batch", [256, 128])
+def test_split_batch_step_agrees_with_single_workgroup(batch, tmp_path):
+    """DTP_GROUPS=1 turns the split-batch step off: the same run on one workgroup per
+    model (the one-lane step at 256, the 2-lanes step at 128) agrees with it to float
+    reassociation."""
+    outs = {}
+    for flag in ("1", "auto"):
+        out = str(tmp_path / f"g{flag}.pt")
+        env = {k: v for k, v in os.environ.items() if k not in ("DTP_LANES", "DTP_GROUPS")}
+        if flag == "1":
+            env["DTP_GROUPS"] = "1"
+        r = subprocess.run([sys.executable, "-c", _FORCE_SCRIPT.format(root=ROOT, batch=batch, out=out)],
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[flag] = torch.load(out, weights_only=True)
+    assert outs["1"]["lanes"] == (1 if batch == 256 else 2) and outs["auto"]["lanes"] == 4
+    torch.testing.assert_close(outs["auto"]["l"], outs["1"]["l"], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(outs["auto"]["p"], outs["1"]["p"], rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("batch", [256, 64])

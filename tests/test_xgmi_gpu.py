@@ -6,11 +6,11 @@ hipGraph-captured all-reduce)."""
 import pytest
 import torch
 
-from distributed_training_pytorch_amd.data.sampler import SamplerGeometry
+from distributed_training_pytorch_amd.data.sampler import EpochIndexStream, SamplerGeometry
 from distributed_training_pytorch_amd.data.toy_data import ToyData
 from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer
-from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC
-from distributed_training_pytorch_amd.ops.optim import OptimConfig
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, MlpSpec, mlp_forward_ref
+from distributed_training_pytorch_amd.ops.optim import OptimConfig, adam_update_ref
 
 from .dist_utils import run_ranks
 from .test_dp_cpu import _init, _reference
@@ -146,3 +146,66 @@ def test_xgmi_selftest_failure_on_one_rank_falls_back_consistently():
         torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=2e-5)
         torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
     assert torch.equal(res[0][0], res[1][0]), "replicas diverged after the fallback"
+
+
+H15 = MlpSpec(2, 15, 5, 1)
+
+
+def _h15_init(seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(H15.P, generator=g) * 0.3 for _ in range(2)]
+
+
+def _h15_rank(rank, world, steps):
+    """MlpSpec(2, 15, 5, 1) (P = 781) at per-rank batch 64: the 4-lanes step owns 4
+    parameters per thread, the layout with the most granules per slot -- the receive
+    buffer must be sized for it (the buffer rsrc does no bounds check)."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, Y = ToyData(n=512, seed=1).device_tensors(dev)
+    geom = SamplerGeometry(n=512, world=world, rank=rank, batch=64, seed=3)
+    tr = FusedTrainer(H15, 2, X, Y, geom, OptimConfig(lr=1e-2), EngineConfig(comm="xgmi", steps_per_launch=4),
+                      init_params=_h15_init(7))
+    assert tr.lanes == 4, tr.lanes
+    tr.train(steps)
+    tr.synchronize()
+    out = (tr.params.cpu(), tr.losses(0, steps), tr.comm)
+    tr.close()
+    return out
+
+
+def _h15_reference(world, steps):
+    ds = ToyData(n=512, seed=1)
+    geoms = [EpochIndexStream(SamplerGeometry(n=512, world=world, rank=r, batch=64, seed=3)) for r in range(world)]
+    params = torch.stack(_h15_init(7)).double()
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    cfg = OptimConfig(lr=1e-2)
+    losses = []
+    for t in range(steps):
+        row = []
+        for i in range(2):
+            gs, ls = [], []
+            for g in geoms:
+                idx = torch.tensor(g.indices(t))
+                p = params[i].clone().requires_grad_(True)
+                loss = torch.nn.functional.mse_loss(mlp_forward_ref(p, H15, ds.X[idx].double()), ds.Y[idx].double())
+                (gr,) = torch.autograd.grad(loss, p)
+                gs.append(gr)
+                ls.append(loss.item())
+            with torch.no_grad():
+                adam_update_ref(params[i], m[i], v[i], torch.stack(gs).mean(0), t + 1, cfg)
+            row.append(sum(ls) / world)
+        losses.append(row)
+    return params.float(), torch.tensor(losses, dtype=torch.float32)
+
+
+def test_two_ranks_h15_lanes_exchange_buffer():
+    steps = 8
+    res = run_ranks(_h15_rank, 2, (steps,), timeout=300)
+    ref_p, ref_l = _h15_reference(2, steps)
+    for r in range(2):
+        p, l, used = res[r]
+        assert used == "xgmi", f"rank {r} fell back to {used}"
+        torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=5e-5)
+        torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
+    assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
