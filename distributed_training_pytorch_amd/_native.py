@@ -238,6 +238,7 @@ def _declare(lib):
         "dtp_train_engine_destroy": (None, [c_void_p]),
         "dtp_train_engine_lanes": (c_int, [c_void_p]),
         "dtp_train_engine_groups": (c_int, [c_void_p]),
+        "dtp_train_engine_profile": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
         "dtp_train_engine_status": (c_int, [c_void_p, P(c_int)]),
         "dtp_mlp_train_lanes": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
         "dtp_mlp_train_profile_lanes": (c_int, [P(TrainArgs), c_int, c_void_p]),

@@ -58,6 +58,9 @@ struct LaneCfg {
   static constexpr int NPR = (NO + 1) / 2;    // v_pk_fma pairs per slice
   static constexpr bool EXACT = NO * L == H;  // every slot of every part is a real unit
   static constexpr int pad4(int x) { return (x + 3) & ~3; }
+  // bf16 compute (Stage BF): matmul operands and outputs rounded to bf16 (mlp_core.h); the
+  // dW tiles stay on the exact fp32 MFMA, whose products of bf16 values are exact
+  static DTP_DEV float rnd(float v) { return S::rnd(v); }
   static constexpr int RW = pad4(H + 1);      // last layer's whole block: row o = W[o][0..H-1], b[o]
   // forward block of partitioned layer l (< NL-1): rows r < din(l) = inputs, row din(l) = bias;
   // a row = [part][NOP] (W[p*NO + k][r] at (r*L + p)*NOP + k)
@@ -217,8 +220,8 @@ DTP_DEV void lane_fwd_layer(const float* wl, const float* wlp, const LFBlk<C, l>
   });
   static_for<0, NO>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
-    const float v = (k & 1) ? z[k / 2].y : z[k / 2].x;
-    st.own[l][k] = fmaxf(v, v * slope);  // LeakyReLU, exact for 0 <= slope <= 1
+    const float v = C::rnd((k & 1) ? z[k / 2].y : z[k / 2].x);  // bf16: the Linear output, then the activation
+    st.own[l][k] = C::rnd(fmaxf(v, v * slope));  // LeakyReLU, exact for 0 <= slope <= 1
   });
   // the whole output vector in every lane of the sample
   static_for<0, C::L>([&](auto PC) {
@@ -265,7 +268,7 @@ DTP_DEV void lane_forward(const float* wl, const float* wlp, const LFBlk<C, l>& 
       lchunk<i, H>(wl, wlp, bt2, none);
       __builtin_amdgcn_sched_barrier(0);
     });
-    static_for<0, C::OUT>([&](auto OC) { out[decltype(OC)::value] = z[decltype(OC)::value]; });
+    static_for<0, C::OUT>([&](auto OC) { out[decltype(OC)::value] = C::rnd(z[decltype(OC)::value]); });
   }
 }
 

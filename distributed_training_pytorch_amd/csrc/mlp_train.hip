@@ -652,8 +652,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     if (NPT * tid + k < P) {
-      sm.wb[pf[k]] = pw[k];
-      if (pb[k] >= 0) sm.wb[pb[k]] = pw[k];
+      const float wv = S::rnd(pw[k]);  // bf16 compute: the matmul operand is the bf16 weight
+      sm.wb[pf[k]] = wv;
+      if (pb[k] >= 0) sm.wb[pb[k]] = wv;
     }
   }
   int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
@@ -662,7 +663,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     di = (unsigned)di < (unsigned)smp.n ? di : 0;
     static_for<0, S::IN>([&](auto IC) {
       constexpr int i = decltype(IC)::value;
-      const float t_ = sm.data[di * S::IN + i];
+      const float t_ = S::rnd(sm.data[di * S::IN + i]);
       x[i] = v ? t_ : 0.f;
     });
     static_for<0, S::OUT>([&](auto JC) {
@@ -742,7 +743,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       constexpr int j = decltype(JC)::value;
       const float d = out[j] - ny[j];
       lpart = valid ? fmaf(d, d, lpart) : lpart;
-      dzl[j] = valid ? 2.f * d * inv : 0.f;
+      dzl[j] = valid ? S::rnd(2.f * d * inv) : 0.f;
     });
     DTP_STAMP(2);
 
@@ -771,8 +772,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       });
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
-        const float v = (k & 1) ? g[k / 2].y : g[k / 2].x;
-        dzp[k] = v * leaky_grad_from_out(st.own[l - 1][k], slope);
+        const float v = S::rnd((k & 1) ? g[k / 2].y : g[k / 2].x);
+        dzp[k] = S::rnd(v * leaky_grad_from_out(st.own[l - 1][k], slope));
       });
       if constexpr (!SC::PACK) {
         __builtin_amdgcn_wave_barrier();
@@ -826,8 +827,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       acc[SC::tile(l)] = a0 + a1;
       static_for<0, NO>([&](auto KC) {
         constexpr int k = decltype(KC)::value;
-        const float v = (k & 1) ? g[k / 2].y : g[k / 2].x;
-        dzp[k] = v * leaky_grad_from_out(st.own[l - 1][k], slope);
+        const float v = S::rnd((k & 1) ? g[k / 2].y : g[k / 2].x);
+        dzp[k] = S::rnd(v * leaky_grad_from_out(st.own[l - 1][k], slope));
       });
     };
     auto hidden_rest = [&](auto self, auto LC, const auto& B) -> void {
@@ -905,8 +906,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const bool own = NPT * tid + k < P;
-        *(own ? &sm.wb[pf[k]] : &sm.sink[0]) = pw[k];
-        *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = pw[k];
+        const float wv = S::rnd(pw[k]);
+        *(own ? &sm.wb[pf[k]] : &sm.sink[0]) = wv;
+        *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = wv;
       }
     }
     if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, NTH) : 0) && a.loss_log && lead) {
@@ -1017,9 +1019,9 @@ void launch_lanes(const DtpTrainArgs& a, hipStream_t st) {
 }
 
 // split-batch step: member k of model m is block m + 8 k (blocks of absent models exit)
-template <class S, int L, int NW>
+template <class S, int L, int NW, bool PROF = false>
 void launch_lanes_grp(const DtpTrainArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, false, NW, true>), dim3(8 * a.groups),
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, PROF, NW, true>), dim3(8 * a.groups),
                      dim3(64 * NW), 0, st, a);
 }
 
@@ -1062,7 +1064,7 @@ int pick_groups(const DtpTrainArgs& a, int mode, const LanePick& lp, bool allow)
     return e ? atoi(e) : 0;
   }();
   static const bool forced_lanes = getenv("DTP_LANES") != nullptr;  // a forced lanes instance runs as asked
-  if (!allow || env == 1 || forced_lanes || mode != DTP_MODE_ADAM || a.bf16 || a.n_models > 8 || a.smp.world != 1)
+  if (!allow || env == 1 || forced_lanes || mode != DTP_MODE_ADAM || a.n_models > 8 || a.smp.world != 1)
     return 1;
   if (a.smp.n * (2 + 1) > dtp::kLaneData) return 1;
   const int b = min(a.smp.batch, a.smp.num_samples);
@@ -1083,7 +1085,7 @@ LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
     return f;
   }();
   LanePick r;
-  if (!fast || a.bf16 || a.smp.n * (in + out) > dtp::kLaneData) return r;
+  if (!fast || a.smp.n * (in + out) > dtp::kLaneData) return r;
   // the largest batch a step sees: a rank's share of the epoch can be smaller than the
   // configured batch (strong scaling: 512 samples over 8 ranks -> 64 of batch 256)
   const int b = min(a.smp.batch, a.smp.num_samples);
@@ -1100,13 +1102,22 @@ TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int ou
                             LanePick* pick = nullptr, bool allow_groups = false) {
   const bool fast = fast_path_ok(a, in, out, mode);
   LanePick lp = pick_lanes(a, in, out, fast);
-  if (fast && in == 2 && h == 10 && nl == 5 && out == 1) {  // the toy shape: split-batch instance
+  const bool toy = in == 2 && h == 10 && nl == 5 && out == 1;
+  if (fast && toy) {  // the toy shape: split-batch instance
     const int gr = pick_groups(a, mode, lp, allow_groups);
     if (gr > 1) {
       lp = LanePick{4, 4, gr};
       if (pick) *pick = lp;
-      return &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false>, 4, 4>;
+      return a.bf16 ? &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false, true>, 4, 4>
+                    : &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false>, 4, 4>;
     }
+  }
+  // bf16 lanes instances: the toy shape, one wave per SIMD
+  if (a.bf16 && (!toy || lp.NW != 4)) lp = LanePick{};
+  if (a.bf16 && lp.L > 1) {
+    using B = dtp::Stage<2, 10, 5, 1, false, true>;
+    if (pick) *pick = lp;
+    return lp.L == 4 ? lanes_fn<B, 4, 4>(mode) : lanes_fn<B, 2, 4>(mode);
   }
   if (pick) *pick = lp;
   if (lp.L > 1 && lp.NW == 4) {
@@ -1297,6 +1308,21 @@ void* dtp_train_engine_create(const DtpTrainArgs* a, int in, int h, int nl, int 
     return nullptr;
   }
   return e;
+}
+
+// diagnostic: the engine's split-batch step (fp32 toy shape) as its PROF instance, phase
+// stamps into prof (u64[8 * groups blocks][8][32], block b = model b % 8, member b / 8)
+int dtp_train_engine_profile(void* h, int n_steps, int t0, void* prof, void* stream) {
+  auto* e = static_cast<TrainEngine*>(h);
+  if (!e || !prof || n_steps <= 0) return set_err(-1, "bad engine profile args");
+  if (e->pick.GR <= 1 || e->a.bf16 || e->mode != DTP_MODE_ADAM)
+    return set_err(-2, "the engine profile instance is the fp32 split-batch step");
+  DtpTrainArgs a = e->a;
+  a.n_steps = n_steps;
+  a.host_t0 = t0;
+  a.status = static_cast<int*>(prof);
+  launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false>, 4, 4, true>(a, (hipStream_t)stream);
+  return check_launch("mlp_train_lanes_kernel<grp, prof>");
 }
 
 // workgroups per model of the engine's step (1, or the split-batch step's group size)

@@ -24,25 +24,34 @@ NAMES = ["step_start", "x_loaded", "fwd+loss", "bwd_done(w0)", "tiles_reduced", 
 
 def main():
     # python scripts/prof_stamps.py [--lanes L --batch B]: L = 2 / 4 stamps the several-lanes step
+    # --groups: the engine's split-batch step (csrc/grp_core.h; the default at batch > 64)
     lanes = int(sys.argv[sys.argv.index("--lanes") + 1]) if "--lanes" in sys.argv else 1
     batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 256
+    grouped = "--groups" in sys.argv
     dev = torch.device("cuda", 0)
     X, Y = ToyData(seed=0).device_tensors(dev)
     tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=batch), cfg=EngineConfig())
     tr.train(50)  # warm
     tr.synchronize()
     lib = nat.load()
-    prof = torch.zeros(2 * 8 * 32, dtype=torch.int64, device=dev)
+    nblk = 8 * max(1, tr.groups) if grouped else 2
+    prof = torch.zeros(nblk * 8 * 32, dtype=torch.int64, device=dev)
     res = {}
     for rep in range(3):
         a = tr._train_args(8, nat.MODE_ADAM, None)
         a.status = nat.ptr(prof)
-        if lanes > 1:
+        if grouped:
+            nat.check(lib.dtp_train_engine_profile(tr._engine_handle(), 8, tr.t, nat.ptr(prof), nat.stream_ptr()),
+                      "engine profile")
+        elif lanes > 1:
             nat.check(lib.dtp_mlp_train_profile_lanes(ctypes.byref(a), lanes, nat.stream_ptr()), "profile")
         else:
             nat.check(lib.dtp_mlp_train_profile(ctypes.byref(a), nat.stream_ptr()), "profile")
         torch.cuda.synchronize()
-        st = prof.view(2, 8, 32).cpu()
+        st = prof.view(nblk, 8, 32).cpu()
+        if grouped:  # per member of model 0 (blocks 0, 8, 16, ...): exchange = tiles_reduced -> grads_summed
+            res.setdefault("members_exchange_cycles", []).append(
+                [[int(st[8 * k, it, 5] - st[8 * k, it, 4]) for it in range(1, 8)] for k in range(tr.groups)])
         rows = []
         for it in range(1, 8):
             s = st[0, it]

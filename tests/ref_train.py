@@ -17,9 +17,12 @@ def loss_fn(out, y, loss: str):
     return F.mse_loss(out, y.view_as(out))
 
 
-def torch_train(spec, init, X, Y, geoms, steps: int, ocfg: OptimConfig, loss: str = "mse"):
+def torch_train(spec, init, X, Y, geoms, steps: int, ocfg: OptimConfig, loss: str = "mse",
+                forward=mlp_forward_ref):
     """init: list of [P] tensors (one per model); geoms: one SamplerGeometry (or any
-    object with .indices(t)) per rank.  Returns (params [n_models, P], losses [steps, n_models])."""
+    object with .indices(t)) per rank; forward: the model (mlp_forward_ref, or the bf16
+    rounding model mlp_forward_ref_bf16).  Returns (params [n_models, P], losses
+    [steps, n_models])."""
     X, Y = X.detach().cpu().double(), Y.detach().cpu()
     params = [torch.nn.Parameter(p.detach().cpu().double().clone()) for p in init]
     opts = [ocfg.torch_optimizer([p]) for p in params]
@@ -31,7 +34,7 @@ def torch_train(spec, init, X, Y, geoms, steps: int, ocfg: OptimConfig, loss: st
             for g in geoms:
                 idx = torch.tensor(g.indices(t), dtype=torch.long)
                 q = p.detach().clone().requires_grad_(True)
-                lo = loss_fn(mlp_forward_ref(q, spec, X[idx]), Y[idx].double() if loss == "mse" else Y[idx], loss)
+                lo = loss_fn(forward(q, spec, X[idx]), Y[idx].double() if loss == "mse" else Y[idx], loss)
                 (gr,) = torch.autograd.grad(lo, q)
                 gs.append(gr)
                 ls.append(lo.item())

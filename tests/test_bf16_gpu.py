@@ -108,3 +108,29 @@ def test_trainer_precision_bf16(tmp_path, engine):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "'global_step': 40" in r.stdout
     assert f"'engine': '{'fused' if engine == 'auto' else 'module'}'" in r.stdout, r.stdout[-1500:]
+
+
+@pytest.mark.parametrize("batch,lanes,groups", [(64, 4, 1), (128, 4, 2), (256, 4, 4)])
+def test_bf16_lanes_and_split_batch_steps_match_rounding_model(batch, lanes, groups):
+    """The bf16 instances of the several-lanes step (per-rank batch <= 64) and of the
+    split-batch step (4-lanes members, 64 samples each) against autograd through the bf16
+    rounding model + torch.optim.Adam.  Accumulation order may move a bf16 value by an ulp
+    (2^-8), hence the bf16 tolerances."""
+    X, Y = ToyData(n=512, seed=4).device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=5)
+    g = torch.Generator().manual_seed(9)
+    init = [torch.randn(TOY_SPEC.P, generator=g) * 0.4 for _ in range(2)]
+    ocfg = OptimConfig(lr=1e-2)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=5, precision="bf16"),
+                      init_params=[p.to(DEV) for p in init])
+    assert (tr.lanes, tr.groups) == (lanes, groups)
+    steps = 10
+    tr.train(steps)
+    tr.synchronize()
+    got_l, got_p = tr.losses(0, steps), tr.params.cpu()
+    tr.close()
+    ref_p, ref_l = torch_train(TOY_SPEC, init, X, Y, [EpochIndexStream(geom)], steps, ocfg, forward=mlp_forward_ref_bf16)
+    torch.testing.assert_close(got_l, ref_l, rtol=2e-2, atol=1e-3)
+    torch.testing.assert_close(got_p, ref_p, rtol=2e-2, atol=2e-3)
+    fp_p, fp_l = torch_train(TOY_SPEC, init, X, Y, [EpochIndexStream(geom)], steps, ocfg)
+    assert not torch.allclose(got_l, fp_l, rtol=1e-6, atol=0)  # bf16 compute for real, not the fp32 kernel
