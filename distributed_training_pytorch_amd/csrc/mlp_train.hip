@@ -568,7 +568,9 @@ struct LaneSmem {
 // the step on batch positions [k 64 NW / L, (k + 1) 64 NW / L), and the members' partial
 // weight gradients and losses are summed on chip before every member's (identical)
 // optimizer step.
-template <class S, int L, int MODE, bool PROF = false, int NW = 4, bool GRP = false>
+// CE: softmax cross-entropy head (class ids as floats in Y) instead of MSE; MODE: Adam or
+// SGD (momentum, weight decay), local or with the in-kernel xGMI exchange.
+template <class S, int L, int MODE, bool PROF = false, int NW = 4, bool GRP = false, bool CE = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
 void mlp_train_lanes_kernel(DtpTrainArgs a) {
   using SC = Scal<S>;
@@ -576,9 +578,12 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   constexpr int NTH = 64 * NW;                 // threads of the workgroup
   constexpr int NPT = (S::P + NTH - 1) / NTH;  // parameters owned per thread (optimizer, exchange)
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NO = C::NO, TS = C::TS, H = S::H;
-  constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM;
-  static_assert(MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM, "the lanes step serves the Adam modes");
+  constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
+  constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
+  static_assert(MODE != DTP_MODE_GRAD, "the lanes step serves the optimizer modes");
   static_assert(!(GRP && kXgmi), "the split-batch step serves one rank");
+  static_assert(!CE || S::OUT >= 2, "cross-entropy needs >= 2 classes");
+  constexpr int YD = CE ? 1 : S::OUT;  // target floats per sample (a class id for CE)
   __shared__ __align__(16) LaneSmem<S, L, NW> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = GRP ? (int)(blockIdx.x & 7u) : (int)blockIdx.x;
@@ -604,10 +609,10 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     const bool own = p < P;
     pw[k] = own ? gp[p] : 0.f;
     mr[k] = own ? a.opt_m[(size_t)model * P + p] : 0.f;
-    vr[k] = own ? a.opt_v[(size_t)model * P + p] : 0.f;
+    vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
   }
   const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
-  const bool htab = a.adam_tab && a.host_t0 >= 0;
+  const bool htab = kAdam && a.adam_tab && a.host_t0 >= 0;
   float2 tabv[kAdamTab / NTH];
   if (htab) adam_tab_load<kAdamTab / NTH, NTH>(a, t0, 0, tid, tabv);
   int epoch = t0 / smp.steps_per_epoch;
@@ -634,7 +639,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   unsigned long long xwait = 0;
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
-  for (int e = tid; e < smp.n * S::OUT; e += NTH) sm.data[smp.n * S::IN + e] = a.Y[e];
+  for (int e = tid; e < smp.n * YD; e += NTH) sm.data[smp.n * S::IN + e] = a.Y[e];
   const int yoff = smp.n * S::IN;
   // this wave's staging areas: zero (unwritten rows / columns stay finite), then the
   // constant-1 bias columns of every tile, written once per launch
@@ -668,7 +673,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     });
     static_for<0, S::OUT>([&](auto JC) {
       constexpr int j = decltype(JC)::value;
-      const float t_ = sm.data[yoff + di * S::OUT + j];
+      const float t_ = j < YD ? sm.data[yoff + di * YD + j] : 0.f;
       y[j] = v ? t_ : 0.f;
     });
     return v;
@@ -689,7 +694,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       sm.adam_tab[e] = make_float2((float)(a.hp.lr / bc1), (float)sqrt(bc2));
     }
   };
-  fill_adam(0);
+  if (kAdam) fill_adam(0);
   // per-lane LDS bases: the part's slice of the partitioned blocks, the sample's slot in a
   // staged operand (+ the part's first column), the MFMA reader's operands
   const float* const wlp = sm.wb + part * C::NOP;
@@ -715,7 +720,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   for (int it = 0; it < a.n_steps; ++it) {
     DTP_STAMP(0);
     const int bsz = min(smp.batch, smp.num_samples - bi * smp.batch);
-    const float inv = 1.f / (float)(bsz * S::OUT);
+    const float inv = CE ? 1.f / (float)bsz : 1.f / (float)(bsz * S::OUT);
     f32x4 acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -739,12 +744,31 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     // ---------------- loss (MSE) -> output gradient (every lane of the sample)
     float dzl[S::OUT];
     float lpart = 0.f;
-    static_for<0, S::OUT>([&](auto JC) {
-      constexpr int j = decltype(JC)::value;
-      const float d = out[j] - ny[j];
-      lpart = valid ? fmaf(d, d, lpart) : lpart;
-      dzl[j] = valid ? S::rnd(2.f * d * inv) : 0.f;
-    });
+    if constexpr (!CE) {
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float d = out[j] - ny[j];
+        lpart = valid ? fmaf(d, d, lpart) : lpart;
+        dzl[j] = valid ? S::rnd(2.f * d * inv) : 0.f;
+      });
+    } else {  // the one-lane kernel's CE arithmetic (mlp_train_kernel), per lane
+      const int cls = valid ? (int)ny[0] : 0;
+      float mx = out[0];
+      static_for<1, S::OUT>([&](auto JC) { mx = fmaxf(mx, out[decltype(JC)::value]); });
+      float se = 0.f, zc = 0.f;
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        se += __expf(out[j] - mx);
+        zc = (j == cls) ? out[j] : zc;
+      });
+      const float lse = mx + __logf(se);
+      const float rs = 1.f / se;
+      lpart = valid ? lse - zc : 0.f;
+      static_for<0, S::OUT>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        dzl[j] = valid ? S::rnd((__expf(out[j] - mx) * rs - (j == cls ? 1.f : 0.f)) * inv) : 0.f;
+      });
+    }
     DTP_STAMP(2);
 
     // ---------------- backward
@@ -867,7 +891,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
         *reinterpret_cast<f32x4*>(&sm.red[wave][tt * SC::TSZ + SC::tslot(4 * q, col)]) = acc[tt];
     }
     __syncthreads();
-    const float2 adam_sc = sm.adam_tab[it % kAdamTab];
+    const float2 adam_sc = kAdam ? sm.adam_tab[it % kAdamTab] : make_float2(0.f, 1.f);
     DTP_STAMP(4);
     float g[NPT];
 #pragma unroll
@@ -901,8 +925,12 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       AdamScalars as = adam_consts(a.hp);
       as.step_size = adam_sc.x;
       as.bc2_sqrt = adam_sc.y;
+      const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
+      for (int k = 0; k < NPT; ++k) {
+        if constexpr (kAdam) adam_update(pw[k], mr[k], vr[k], g[k] * a.hp.grad_scale, as);
+        else sgd_update(pw[k], mr[k], g[k] * a.hp.grad_scale, lr, mom, wd, t0 + it == 0);
+      }
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const bool own = NPT * tid + k < P;
@@ -917,7 +945,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     }
     DTP_STAMP(6);
     __syncthreads();
-    if ((it + 1) % kAdamTab == 0 && it + 1 < a.n_steps) {
+    if (kAdam && (it + 1) % kAdamTab == 0 && it + 1 < a.n_steps) {
       fill_adam(it + 1);
       __syncthreads();
     }
@@ -931,7 +959,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     if (p < P) {
       gp[p] = pw[k];
       a.opt_m[(size_t)model * P + p] = mr[k];
-      a.opt_v[(size_t)model * P + p] = vr[k];
+      if (kAdam) a.opt_v[(size_t)model * P + p] = vr[k];
     }
   }
   if (tid == 0) a.step[model] = t0 + a.n_steps;
@@ -989,22 +1017,28 @@ TrainLaunchFn train_fn(int mode, bool fast) {
   }
 }
 
-// may this launch take the FAST instance?  (the kernel's FAST preconditions)
-bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
+// the FAST preconditions on the data path (the kernels' compile-time configuration): the
+// SAMPLER_TABLE ring, the dataset cached in LDS, 0 <= slope <= 1, batch <= kBlock.  The
+// several-lanes and split-batch steps need these, for every loss and optimizer they serve.
+bool fast_base_ok(const DtpTrainArgs& a, int in, int out) {
   static const bool disabled = [] {
     const char* e = getenv("DTP_FAST");
     return e && e[0] == '0';
   }();
-  if (disabled || (mode != DTP_MODE_ADAM && mode != DTP_MODE_XGMI_ADAM)) return false;
+  if (disabled) return false;
   const dtp::SamplerCfg& s = a.smp;
   const int ydim = a.loss == DTP_LOSS_CE ? 1 : out;
   // n >= world: the FAST gather wraps a padded-list position with ONE subtraction of n
   // (positions stay below n + world - 1), where the generic sampler takes q % n
   const bool ring = s.perm && s.perm_epochs > 0 && (s.perm_epochs & (s.perm_epochs - 1)) == 0;
-  return a.cache_data && a.loss == DTP_LOSS_MSE && min(s.batch, s.num_samples) <= dtp::kBlock &&
-         s.mode == dtp::SAMPLER_TABLE && ring &&
-         s.n >= s.world && s.n * (in + ydim) <= dtp::kDataCache &&
-         a.hp.slope >= 0.f && a.hp.slope <= 1.f;
+  return a.cache_data && min(s.batch, s.num_samples) <= dtp::kBlock && s.mode == dtp::SAMPLER_TABLE && ring &&
+         s.n >= s.world && s.n * (in + ydim) <= dtp::kDataCache && a.hp.slope >= 0.f && a.hp.slope <= 1.f;
+}
+
+// may this launch take the one-lane FAST instance?  (the data-path preconditions, Adam, MSE)
+bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
+  return fast_base_ok(a, in, out) && (mode == DTP_MODE_ADAM || mode == DTP_MODE_XGMI_ADAM) &&
+         a.loss == DTP_LOSS_MSE;
 }
 
 // shapes with a bf16-compute instance (the toy model: MSE and CE heads)
@@ -1012,24 +1046,81 @@ bool fast_path_ok(const DtpTrainArgs& a, int in, int out, int mode) {
   X(2, 10, 5, 1)                 \
   X(2, 10, 5, 4)
 
-template <class S, int L, int MODE, int NW>
+template <class S, int L, int MODE, int NW, bool CE = false>
 void launch_lanes(const DtpTrainArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, MODE, false, NW>), dim3(a.n_models), dim3(64 * NW), 0, st,
-                     a);
-}
-
-// split-batch step: member k of model m is block m + 8 k (blocks of absent models exit)
-template <class S, int L, int NW, bool PROF = false>
-void launch_lanes_grp(const DtpTrainArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, DTP_MODE_ADAM, PROF, NW, true>), dim3(8 * a.groups),
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, MODE, false, NW, false, CE>), dim3(a.n_models),
                      dim3(64 * NW), 0, st, a);
 }
 
-template <class S, int L, int NW>
-TrainLaunchFn lanes_fn(int mode) {
-  if (mode == DTP_MODE_ADAM) return &launch_lanes<S, L, DTP_MODE_ADAM, NW>;
-  if (mode == DTP_MODE_XGMI_ADAM) return &launch_lanes<S, L, DTP_MODE_XGMI_ADAM, NW>;
+// split-batch step: member k of model m is block m + 8 k (blocks of absent models exit)
+template <class S, int L, int NW, bool PROF = false, int MODE = DTP_MODE_ADAM, bool CE = false>
+void launch_lanes_grp(const DtpTrainArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((dtp::mlp_train_lanes_kernel<S, L, MODE, PROF, NW, true, CE>), dim3(8 * a.groups),
+                     dim3(64 * NW), 0, st, a);
+}
+
+// the lanes instances of one (shape, L, NW, loss, optimizer family)
+template <class S, int L, int NW, bool CE, bool SGD>
+TrainLaunchFn lanes_modes(int mode) {
+  if constexpr (!SGD) {
+    if (mode == DTP_MODE_ADAM) return &launch_lanes<S, L, DTP_MODE_ADAM, NW, CE>;
+    if (mode == DTP_MODE_XGMI_ADAM) return &launch_lanes<S, L, DTP_MODE_XGMI_ADAM, NW, CE>;
+  } else {
+    if (mode == DTP_MODE_SGD) return &launch_lanes<S, L, DTP_MODE_SGD, NW, CE>;
+    if (mode == DTP_MODE_XGMI_SGD) return &launch_lanes<S, L, DTP_MODE_XGMI_SGD, NW, CE>;
+  }
   return nullptr;
+}
+template <class S, int NW, bool CE, bool SGD>
+TrainLaunchFn lanes_by_l(int L, int mode) {
+  return L == 4 ? lanes_modes<S, 4, NW, CE, SGD>(mode) : lanes_modes<S, 2, NW, CE, SGD>(mode);
+}
+
+// Instances of the several-lanes step (nullptr: none -> the one-lane kernel).  Adam + MSE
+// for every DTP_TRAIN_SHAPES shape; SGD + MSE for the toy shape; the CE head (2,10,5,4) with
+// Adam and SGD; bf16: the toy shape, Adam + MSE; two waves per SIMD: toy, Adam + MSE.
+TrainLaunchFn lanes_inst(int in, int h, int nl, int out, int L, int NW, int mode, bool ce, bool bf16) {
+  const bool sgd = mode == DTP_MODE_SGD || mode == DTP_MODE_XGMI_SGD;
+  const bool toy = in == 2 && h == 10 && nl == 5 && out == 1;
+  const bool ce4 = in == 2 && h == 10 && nl == 5 && out == 4;
+  if (L != 2 && L != 4) return nullptr;
+  if (NW == 8) {
+    if (!toy || ce || sgd || bf16) return nullptr;
+    return lanes_by_l<dtp::Stage<2, 10, 5, 1, false>, 8, false, false>(L, mode);
+  }
+  if (NW != 4) return nullptr;
+  if (bf16) return (toy && !ce && !sgd) ? lanes_by_l<dtp::Stage<2, 10, 5, 1, false, true>, 4, false, false>(L, mode)
+                                        : nullptr;
+  if (ce) {
+    if (!ce4) return nullptr;
+    using T = dtp::Stage<2, 10, 5, 4, false>;
+    return sgd ? lanes_by_l<T, 4, true, true>(L, mode) : lanes_by_l<T, 4, true, false>(L, mode);
+  }
+  if (sgd) return toy ? lanes_by_l<dtp::Stage<2, 10, 5, 1, false>, 4, false, true>(L, mode) : nullptr;
+#define X(I, H, N, O) \
+  if (in == I && h == H && nl == N && out == O) return lanes_by_l<dtp::Stage<I, H, N, O, false>, 4, false, false>(L, mode);
+  DTP_TRAIN_SHAPES(X)
+#undef X
+  return nullptr;
+}
+
+// Instances of the split-batch step (4-lanes members, one rank): toy fp32 with Adam or SGD,
+// toy bf16 with Adam, the CE head with Adam or SGD
+TrainLaunchFn grp_inst(int in, int h, int nl, int out, int mode, bool ce, bool bf16) {
+  const bool toy = in == 2 && h == 10 && nl == 5 && out == 1;
+  const bool ce4 = in == 2 && h == 10 && nl == 5 && out == 4;
+  using T = dtp::Stage<2, 10, 5, 1, false>;
+  using C4 = dtp::Stage<2, 10, 5, 4, false>;
+  if (mode != DTP_MODE_ADAM && mode != DTP_MODE_SGD) return nullptr;
+  const bool sgd = mode == DTP_MODE_SGD;
+  if (bf16) return (toy && !ce && !sgd) ? &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false, true>, 4, 4> : nullptr;
+  if (ce) {
+    if (!ce4) return nullptr;
+    return sgd ? &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_SGD, true>
+               : &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_ADAM, true>;
+  }
+  if (!toy) return nullptr;
+  return sgd ? &launch_lanes_grp<T, 4, 4, false, DTP_MODE_SGD> : &launch_lanes_grp<T, 4, 4>;
 }
 
 // the step instance of a launch: lanes per sample and waves per workgroup
@@ -1058,17 +1149,16 @@ int xgmi_max_slot16(int P) {
 // Split-batch step (engine launches only: it owns the exchange buffer): a per-rank batch
 // above 64 on one rank runs on ceil(batch / 64) workgroups per model, each the 4-lanes step
 // on 64 samples, their gradients summed on chip.  DTP_GROUPS=1 turns it off (A/B runs).
-int pick_groups(const DtpTrainArgs& a, int mode, const LanePick& lp, bool allow) {
+int pick_groups(const DtpTrainArgs& a, int in, int out, bool allow) {
   static const int env = [] {
     const char* e = getenv("DTP_GROUPS");
     return e ? atoi(e) : 0;
   }();
   static const bool forced_lanes = getenv("DTP_LANES") != nullptr;  // a forced lanes instance runs as asked
-  if (!allow || env == 1 || forced_lanes || mode != DTP_MODE_ADAM || a.n_models > 8 || a.smp.world != 1)
-    return 1;
-  if (a.smp.n * (2 + 1) > dtp::kLaneData) return 1;
+  if (!allow || env == 1 || forced_lanes || a.n_models > 8 || a.smp.world != 1) return 1;
+  if (a.smp.n * (in + out) > dtp::kLaneData) return 1;
   const int b = min(a.smp.batch, a.smp.num_samples);
-  if (b <= 64 || lp.L == 0) return 1;
+  if (b <= 64) return 1;
   const int gr = (b + 63) / 64;
   return gr <= dtp::kGrpMax ? gr : 1;
 }
@@ -1100,37 +1190,24 @@ LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
 
 TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode,
                             LanePick* pick = nullptr, bool allow_groups = false) {
+  const bool base = fast_base_ok(a, in, out);
   const bool fast = fast_path_ok(a, in, out, mode);
-  LanePick lp = pick_lanes(a, in, out, fast);
-  const bool toy = in == 2 && h == 10 && nl == 5 && out == 1;
-  if (fast && toy) {  // the toy shape: split-batch instance
-    const int gr = pick_groups(a, mode, lp, allow_groups);
+  const bool ce = a.loss == DTP_LOSS_CE;
+  LanePick lp = pick_lanes(a, in, out, base);
+  if (base) {
+    const int gr = pick_groups(a, in, out, allow_groups);
     if (gr > 1) {
-      lp = LanePick{4, 4, gr};
-      if (pick) *pick = lp;
-      return a.bf16 ? &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false, true>, 4, 4>
-                    : &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false>, 4, 4>;
+      if (TrainLaunchFn f = grp_inst(in, h, nl, out, mode, ce, a.bf16)) {
+        if (pick) *pick = LanePick{4, 4, gr};
+        return f;
+      }
     }
-  }
-  // bf16 lanes instances: the toy shape, one wave per SIMD
-  if (a.bf16 && (!toy || lp.NW != 4)) lp = LanePick{};
-  if (a.bf16 && lp.L > 1) {
-    using B = dtp::Stage<2, 10, 5, 1, false, true>;
-    if (pick) *pick = lp;
-    return lp.L == 4 ? lanes_fn<B, 4, 4>(mode) : lanes_fn<B, 2, 4>(mode);
-  }
-  if (pick) *pick = lp;
-  if (lp.L > 1 && lp.NW == 4) {
-#define X(I, H, N, O)                                                                                   \
-  if (in == I && h == H && nl == N && out == O)                                                         \
-    return lp.L == 4 ? lanes_fn<dtp::Stage<I, H, N, O, false>, 4, 4>(mode)                              \
-                     : lanes_fn<dtp::Stage<I, H, N, O, false>, 2, 4>(mode);
-    DTP_TRAIN_SHAPES(X)
-#undef X
-  }
-  if (lp.L > 1 && lp.NW == 8 && in == 2 && h == 10 && nl == 5 && out == 1) {  // two waves per SIMD: toy shape
-    using T = dtp::Stage<2, 10, 5, 1, false>;
-    return lp.L == 4 ? lanes_fn<T, 4, 8>(mode) : lanes_fn<T, 2, 8>(mode);
+    if (lp.L > 1) {
+      if (TrainLaunchFn f = lanes_inst(in, h, nl, out, lp.L, lp.NW, mode, ce, a.bf16)) {
+        if (pick) *pick = lp;
+        return f;
+      }
+    }
   }
   if (pick) *pick = LanePick{};
   if (a.bf16) {

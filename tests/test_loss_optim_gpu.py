@@ -134,3 +134,27 @@ def test_rccl_path_sgd_single_rank():
     assert used == "rccl"
     torch.testing.assert_close(l, rl, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(p, rp, rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("batch,groups", [(64, 1), (128, 2), (256, 4)])
+@pytest.mark.parametrize("loss,optim", [("mse", "sgd"), ("ce", "adam"), ("ce", "sgd")])
+def test_lanes_and_split_batch_loss_optim(batch, groups, loss, optim):
+    """SGD (momentum, weight decay) and cross-entropy on the fast steps: the 4-lanes step
+    at per-rank batch 64 and the split-batch step (64 samples per workgroup, batch / 64
+    workgroups per model) above it, against autograd + torch.optim."""
+    spec = CE_SPEC if loss == "ce" else TOY_SPEC
+    ocfg = OptimConfig("sgd", 5e-2, momentum=0.9, weight_decay=1e-4) if optim == "sgd" else OptimConfig(lr=1e-2)
+    ds = _data(loss)
+    X, Y = ds.device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=batch, seed=11)
+    tr = FusedTrainer(spec, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=4, loss=loss),
+                      init_params=[p.to(DEV) for p in _init(spec, 100)])
+    assert (tr.lanes, tr.groups) == (4, groups)
+    steps = 11
+    tr.train(steps)
+    tr.synchronize()
+    p, l = tr.params.cpu(), tr.losses(0, steps)
+    tr.close()
+    rp, rl = _expect(spec, loss, ocfg, steps, batch=batch)
+    torch.testing.assert_close(l, rl, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(p, rp, rtol=1e-3, atol=3e-5)
