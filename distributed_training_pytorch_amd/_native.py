@@ -425,13 +425,46 @@ def native_enabled() -> bool:
     return os.environ.get("DTP_NATIVE", "1") != "0"
 
 
+# streams this module created (raw handle, device index): destroyed at interpreter exit,
+# while the HIP runtime is still loaded -- a stream left to the runtime's own teardown
+# (its static destructors, after Python has gone) was the suspect of an exit-time
+# SIGSEGV in __cxa_finalize under rocprofv3 (profiles/r4_split_streams/README.md)
+_owned_streams: list = []
+_atexit_registered = False
+
+
+def _own_stream(handle: int, device: torch.device) -> None:
+    global _atexit_registered
+    _owned_streams.append((handle, device.index if device.index is not None else torch.cuda.current_device()))
+    if not _atexit_registered:
+        import atexit
+
+        atexit.register(destroy_owned_streams)
+        _atexit_registered = True
+
+
+def destroy_owned_streams() -> None:
+    """Synchronise and destroy every stream made by :func:`priority_stream` /
+    :func:`cu_masked_stream` (idempotent; registered with atexit)."""
+    if not _owned_streams or _lib is None:
+        return
+    while _owned_streams:
+        h, dev = _owned_streams.pop()
+        try:
+            with torch.cuda.device(dev):
+                _lib.dtp_stream_destroy(ctypes.c_void_p(h))
+        except Exception:  # noqa: BLE001 - teardown is best effort
+            pass
+
+
 def priority_stream(device, priority: int) -> "torch.cuda.ExternalStream":
     """A torch stream at a HIP stream priority (``hipStreamCreateWithPriority``, lower =
-    higher priority); it lives for the rest of the process."""
+    higher priority); destroyed at interpreter exit (:func:`destroy_owned_streams`)."""
     lib = require(torch.device(device))
     out = ctypes.c_void_p()
     with torch.cuda.device(torch.device(device)):
         check(lib.dtp_stream_create_priority(int(priority), ctypes.byref(out)), "dtp_stream_create_priority")
+    _own_stream(out.value, torch.device(device))
     return torch.cuda.ExternalStream(out.value, device=torch.device(device))
 
 
@@ -446,7 +479,7 @@ def stream_priority_levels(device) -> list[int]:
 
 def cu_masked_stream(device, cus) -> "torch.cuda.ExternalStream":
     """A torch stream whose kernels run only on the listed logical CUs
-    (``hipExtStreamCreateWithCUMask``); it lives for the rest of the process."""
+    (``hipExtStreamCreateWithCUMask``); destroyed at interpreter exit."""
     lib = require(torch.device(device))
     cus = sorted(set(int(c) for c in cus))
     if not cus or cus[0] < 0:
@@ -457,4 +490,5 @@ def cu_masked_stream(device, cus) -> "torch.cuda.ExternalStream":
         mask[c // 32] |= 1 << (c % 32)
     out = ctypes.c_void_p()
     check(lib.dtp_stream_create_cu_mask(mask, words, ctypes.byref(out)), "dtp_stream_create_cu_mask")
+    _own_stream(out.value, torch.device(device))
     return torch.cuda.ExternalStream(out.value, device=torch.device(device))

@@ -581,7 +581,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   constexpr bool kXgmi = MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD;
   constexpr bool kAdam = MODE == DTP_MODE_ADAM || MODE == DTP_MODE_XGMI_ADAM;
   static_assert(MODE != DTP_MODE_GRAD, "the lanes step serves the optimizer modes");
-  static_assert(!(GRP && kXgmi), "the split-batch step serves one rank");
+  // GRP with kXgmi: ONE flat exchange over world x groups members (xgmi_core.h)
   static_assert(!CE || S::OUT >= 2, "cross-entropy needs >= 2 classes");
   constexpr int YD = CE ? 1 : S::OUT;  // target floats per sample (a class id for CE)
   __shared__ __align__(16) LaneSmem<S, L, NW> sm;
@@ -635,7 +635,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   const int fidx0 = fast_index(epoch, bi);
   roll(e2, b2);
   int fidx = fast_index(e2, b2);
-  unsigned xepoch = kXgmi ? a.epoch[model] : (GRP ? a.grp_epoch[model] : 0u);
+  unsigned xepoch = kXgmi ? a.epoch[model] : (GRP ? a.grp_epoch[model] : 0u);  // GRP + xGMI: the xGMI epochs
   unsigned long long xwait = 0;
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
@@ -904,16 +904,17 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     float lsum = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::losspos()];
-    if constexpr (GRP) {  // the members' partial sums, on chip (grp_core.h)
+    if constexpr (GRP && !kXgmi) {  // the members' partial sums, on chip (grp_core.h)
       xepoch += 1u;
       lsum = grp_allreduce<NPT, NTH>(gctx, model, P, g, lsum, xepoch, tid);
     }
-    const float mean_loss = lsum * inv;
+    const float mean_loss = lsum * inv;  // GRP + xGMI: this member's share of the rank's mean
     DTP_STAMP(5);
     float gloss = mean_loss;
     if constexpr (kXgmi) {
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr);
+      gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
+                                             GRP ? a.groups : 1, gk);
     }
     const int lslot_now = lslot;
     roll(epoch, bi);
@@ -964,7 +965,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   }
   if (tid == 0) a.step[model] = t0 + a.n_steps;
   if (kXgmi && tid == 0) a.epoch[model] = xepoch;
-  if (GRP && tid == 0) a.grp_epoch[model] = xepoch;
+  if (GRP && !kXgmi && tid == 0) a.grp_epoch[model] = xepoch;
   if (DTP_XWAIT && kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
 }
 
@@ -1104,23 +1105,37 @@ TrainLaunchFn lanes_inst(int in, int h, int nl, int out, int L, int NW, int mode
   return nullptr;
 }
 
-// Instances of the split-batch step (4-lanes members, one rank): toy fp32 with Adam or SGD,
-// toy bf16 with Adam, the CE head with Adam or SGD
+// Instances of the split-batch step (4-lanes members; one rank, or several with the flat
+// xGMI exchange): toy fp32 with Adam or SGD, toy bf16 with Adam, the CE head with Adam or SGD
 TrainLaunchFn grp_inst(int in, int h, int nl, int out, int mode, bool ce, bool bf16) {
   const bool toy = in == 2 && h == 10 && nl == 5 && out == 1;
   const bool ce4 = in == 2 && h == 10 && nl == 5 && out == 4;
   using T = dtp::Stage<2, 10, 5, 1, false>;
   using C4 = dtp::Stage<2, 10, 5, 4, false>;
-  if (mode != DTP_MODE_ADAM && mode != DTP_MODE_SGD) return nullptr;
-  const bool sgd = mode == DTP_MODE_SGD;
-  if (bf16) return (toy && !ce && !sgd) ? &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false, true>, 4, 4> : nullptr;
+  using B = dtp::Stage<2, 10, 5, 1, false, true>;
+  if (mode == DTP_MODE_GRAD) return nullptr;
+  const bool sgd = mode == DTP_MODE_SGD || mode == DTP_MODE_XGMI_SGD;
+  const bool xg = mode == DTP_MODE_XGMI_ADAM || mode == DTP_MODE_XGMI_SGD;
+  if (bf16) {
+    if (!toy || ce || sgd) return nullptr;
+    return xg ? &launch_lanes_grp<B, 4, 4, false, DTP_MODE_XGMI_ADAM> : &launch_lanes_grp<B, 4, 4>;
+  }
   if (ce) {
     if (!ce4) return nullptr;
-    return sgd ? &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_SGD, true>
-               : &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_ADAM, true>;
+    switch (mode) {
+      case DTP_MODE_ADAM: return &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_ADAM, true>;
+      case DTP_MODE_SGD: return &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_SGD, true>;
+      case DTP_MODE_XGMI_ADAM: return &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_XGMI_ADAM, true>;
+      default: return &launch_lanes_grp<C4, 4, 4, false, DTP_MODE_XGMI_SGD, true>;
+    }
   }
   if (!toy) return nullptr;
-  return sgd ? &launch_lanes_grp<T, 4, 4, false, DTP_MODE_SGD> : &launch_lanes_grp<T, 4, 4>;
+  switch (mode) {
+    case DTP_MODE_ADAM: return &launch_lanes_grp<T, 4, 4>;
+    case DTP_MODE_SGD: return &launch_lanes_grp<T, 4, 4, false, DTP_MODE_SGD>;
+    case DTP_MODE_XGMI_ADAM: return &launch_lanes_grp<T, 4, 4, false, DTP_MODE_XGMI_ADAM>;
+    default: return &launch_lanes_grp<T, 4, 4, false, DTP_MODE_XGMI_SGD>;
+  }
 }
 
 // the step instance of a launch: lanes per sample and waves per workgroup
@@ -1155,12 +1170,14 @@ int pick_groups(const DtpTrainArgs& a, int in, int out, bool allow) {
     return e ? atoi(e) : 0;
   }();
   static const bool forced_lanes = getenv("DTP_LANES") != nullptr;  // a forced lanes instance runs as asked
-  if (!allow || env == 1 || forced_lanes || a.n_models > 8 || a.smp.world != 1) return 1;
+  if (!allow || env == 1 || forced_lanes || a.n_models > 8) return 1;
   if (a.smp.n * (in + out) > dtp::kLaneData) return 1;
   const int b = min(a.smp.batch, a.smp.num_samples);
   if (b <= 64) return 1;
   const int gr = (b + 63) / 64;
-  return gr <= dtp::kGrpMax ? gr : 1;
+  // several ranks: one flat exchange over world x groups virtual members (xgmi_core.h)
+  const int cap = a.smp.world == 1 ? dtp::kGrpMax : dtp::kXgmiMaxWorld / a.smp.world;
+  return gr <= cap ? gr : 1;
 }
 
 LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
@@ -1231,7 +1248,7 @@ int check_xbuf(const DtpTrainArgs& a, int in, int h, int nl, int out, int mode, 
   int P = 0;
   for (int l = 0; l < nl; ++l) P += (l == nl - 1 ? out : h) * ((l == 0 ? in : h) + 1);
   const int nth = lp.L > 1 ? 64 * lp.NW : dtp::kBlock;
-  const long long need = xgmi_bytes_for(P, a.n_models, a.smp.world, xgmi_slot16_threads(P, nth));
+  const long long need = xgmi_bytes_for(P, a.n_models, a.smp.world * lp.GR, xgmi_slot16_threads(P, nth));
   if (need > a.xbuf_bytes) {
     char m[160];
     snprintf(m, sizeof m, "xGMI receive buffer too small: %lld bytes needed, %d allocated", need, a.xbuf_bytes);
@@ -1342,8 +1359,10 @@ int dtp_mlp_workspace_floats(int in, int h, int nl, int out) {
 // ([parity 2][model][src rank][slot] of 16-byte granules, xgmi_core.h)
 long long dtp_xgmi_fused_buffer_bytes(int P, int n_models, int world) {
   // sized for the instance with the most granules: xgmi_slot16 is not monotone in the
-  // parameters per thread, so take the max over every instantiated thread count
-  return xgmi_bytes_for(P, n_models, world, xgmi_max_slot16(P));
+  // parameters per thread, so take the max over every instantiated thread count; and for
+  // the split-batch step's virtual members (world x groups <= kXgmiMaxWorld slots)
+  const int slots = world <= dtp::kXgmiMaxWorld ? dtp::kXgmiMaxWorld : world;
+  return xgmi_bytes_for(P, n_models, slots, xgmi_max_slot16(P));
 }
 
 int dtp_mlp_param_count(int in, int h, int nl, int out) {

@@ -100,11 +100,16 @@ struct XgmiCtx {
 // waited (nullable): += s_memrealtime ticks (100 MHz) from this thread's last publish
 // store to its last granule accepted -- the exchange-wait diagnostic of the bench
 // (status words [4..8), written back once per launch by the caller)
+// GR > 1 (the split-batch step, grp_core.h): every rank runs the step on GR workgroups per
+// model, and the exchange is ONE flat all-reduce over V = W GR virtual members -- member k
+// of rank R is slot R GR + k of every receive buffer, stored once into each rank's buffer
+// (its own rank's too: the other local members read it there), so the on-chip partial sums
+// and the cross-GPU sum cost one hop, not two.  Sums run in slot order (rank-major).
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g)[NPT], float loss, unsigned epoch,
-                                   int tid, unsigned long long* waited = nullptr) {
+                                   int tid, unsigned long long* waited = nullptr, int GR = 1, int gk = 0) {
   constexpr int GPT = xgmi_gpt<NPT>();
-  const int W = a.world, R = a.rank;
+  const int W = a.world * GR, R = a.rank * GR + gk;  // virtual members (slots) and this member's slot
   const int slot = xgmi_slot16(P, NPT);
   const int nthr = xgmi_nthr(P, NPT);
   const int ltid = xgmi_loss_tid<NPT>(P, NTHREADS);
@@ -122,9 +127,10 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   v[GPT][1] = 0.f;
   auto gidx = [&](int k) { return k < GPT ? tid * GPT + k : nthr * GPT; };  // granule index in a slot
   auto mine_k = [&](int k) { return k < GPT ? has_g : has_l; };
-  // publish to every peer (posted xGMI writes; our own slot stays in registers)
-  for (int r = 0; r < W; ++r) {
-    if (r == R) continue;
+  // publish to every rank that has a reader of this slot (posted xGMI writes; our own
+  // contribution stays in registers)
+  for (int r = 0; r < a.world; ++r) {
+    if (r == a.rank && GR == 1) continue;
     const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(a.peers[r]);
 #pragma unroll
     for (int k = 0; k <= GPT; ++k) {
@@ -136,7 +142,7 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   }
   // consume every peer's granules from our local buffer: all pending ones requested
   // at once, only the missing ones re-polled; bounded by the deadline
-  const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[R]);
+  const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[a.rank]);
   const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
   const unsigned long long deadline = t_pub + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
   bool dead = a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
@@ -246,9 +252,10 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
 
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
-                                   unsigned epoch, int tid, unsigned long long* waited = nullptr) {
+                                   unsigned epoch, int tid, unsigned long long* waited = nullptr, int GR = 1,
+                                   int gk = 0) {
   const XgmiCtx c{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
-  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid, waited);
+  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid, waited, GR, gk);
 }
 
 // the fused step's exchange diagnostics in the status block, for model 0's workgroup:

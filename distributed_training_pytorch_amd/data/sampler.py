@@ -15,7 +15,9 @@ as the reference uses them (``demo.py:139-154``):
 """
 from __future__ import annotations
 
+import atexit
 import math
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -288,6 +290,15 @@ def randperm_torch(n: int, seed: int) -> list[int]:
     return torch.randperm(n, generator=g).tolist()
 
 
+_live_rings: "weakref.WeakSet" = weakref.WeakSet()  # rings with a generator thread started
+
+
+@atexit.register
+def _join_ring_threads() -> None:
+    for r in list(_live_rings):
+        r.close()
+
+
 class PermutationRing:
     """Device ring of upcoming epoch permutations for the SAMPLER_TABLE sampler.
 
@@ -362,7 +373,17 @@ class PermutationRing:
                 self._ahead = (e0, count, blk)
 
         self._thread = threading.Thread(target=work, daemon=True)
+        _live_rings.add(self)
         self._thread.start()
+
+    def close(self) -> None:
+        """Wait for the background generator (it may be inside the native randperm): a
+        daemon thread still running native code when the interpreter exits is killed
+        mid-call while the library unloads.  Idempotent; also run at exit."""
+        t, self._thread = self._thread, None
+        if t is not None:
+            t.join()
+        _live_rings.discard(self)
 
     # ---------------------------------------------------------------- residency
     def _write(self, e0: int, host: torch.Tensor) -> None:

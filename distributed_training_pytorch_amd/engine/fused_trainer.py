@@ -257,7 +257,7 @@ class FusedTrainer:
             for _ in range(2):
                 restore()
                 try:
-                    self._launch(1)
+                    self._run_engine(1)  # the engine's own instance (the split-batch step included)
                     torch.cuda.synchronize(self.device)
                 except Exception as e:
                     errs.append(f"launch: {e}")
@@ -600,6 +600,8 @@ class FusedTrainer:
                 comm_util.barrier(self.group)
             self._xgmi.close()
             self._xgmi = None
+        if self._ring is not None:
+            self._ring.close()
 
 
 class LossReadback:

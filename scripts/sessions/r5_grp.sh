@@ -10,4 +10,5 @@ timeout -k 10 150 python bench.py --steps 20 --warmup 5 > $O/bench_k20.json 2>> 
 timeout -k 10 150 python scripts/prof_stamps.py --groups --batch 256 > $O/stamps_grp.log 2>&1 || exit $?
 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_lanes_gpu.py > $O/lanes.log 2>&1 || exit $?
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_bf16_gpu.py > $O/bf16.log 2>&1 || exit $?
-timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_loss_optim_gpu.py > $O/lossopt.log 2>&1
+timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_loss_optim_gpu.py > $O/lossopt.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_xgmi_gpu.py tests/test_bench_gpu.py > $O/xgmi_bench.log 2>&1

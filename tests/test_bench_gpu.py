@@ -88,8 +88,10 @@ def test_bench_strong_scaling_share_gpu(world):
     assert rec["config"]["dataset_samples"] == 512
     assert rec["config"]["global_batch"] == 512
     assert rec["config"]["per_rank_batch"] == 512 // world
-    # per-rank batch 256 / 128 / 64: the one-lane step, then the 2- and 4-lanes steps
-    assert rec["config"]["lanes_per_sample"] == {2: 1, 4: 2, 8: 4}[world], rec["config"]
+    # per-rank batch 256 / 128 / 64: the 4-lanes step on 4 / 2 / 1 workgroups per model (the
+    # split-batch members join the xGMI exchange as world x groups virtual members)
+    assert rec["config"]["lanes_per_sample"] == 4, rec["config"]
+    assert rec["config"]["workgroups_per_model"] == {2: 4, 4: 2, 8: 1}[world], rec["config"]
     # the multi-GPU diagnostics of the line: no fallback, exchange wait and compute split
     assert rec["comm_fallback_reason"] is None
     assert len(rec["exchange_wait_us_per_step_by_rank"]) == world
@@ -98,6 +100,19 @@ def test_bench_strong_scaling_share_gpu(world):
     ref = _single_process_full_batch_losses(steps + warmup)
     for got, want in zip(rec["final_loss"], ref):
         assert abs(got - want) <= 1e-3 * abs(want) + 1e-5, (rec["final_loss"], ref)
+
+
+def test_bench_self_launch_share_gpu():
+    """No torchrun around bench.py: --gpus 2 starts its own two ranks (the driver's N-GPU
+    call shape), here both on the one GPU."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu", "--steps", "20", "--warmup", "5"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["comm"] == "xgmi" and rec["value"] > 0
 
 
 def test_bench_weak_scaling_flag_share_gpu():
