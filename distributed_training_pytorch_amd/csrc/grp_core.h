@@ -50,10 +50,25 @@ struct GrpCtx {
   int GR, k, n_models, timeout_us;
 };
 
+// diagnostic (PROF instances only): s_memtime when the publish stores were issued, when the
+// first poll was consumed and when the last granule arrived, and the number of polls
+struct GrpProf {
+  unsigned long long t_pub, t_first, t_end;
+  unsigned polls;
+};
+
+DTP_DEV unsigned long long grp_clock() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 // g (in): this member's partial sums of its NPT owned parameters; out: the sum over the
 // GR members.  Returns the summed loss partial.  Called by every thread of the member.
 template <int NPT, int NTHREADS>
-DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], float loss, unsigned epoch, int tid) {
+// dead: the caller's sticky timeout flag (read from the status word once per launch)
+DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                            bool& dead, GrpProf* prof = nullptr) {
   constexpr int GPT = xgmi_gpt<NPT>();
   const int slot = grp_slot16(P, NPT);
   const int nthr = xgmi_nthr(P, NPT);
@@ -92,7 +107,7 @@ DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], 
       if (r < c.GR && r != c.k && mine_k(k)) pending |= 1ull << (r * (GPT + 1) + k);
     }
   }
-  bool dead = c.status ? (__hip_atomic_load(&c.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
+  if (prof) prof->t_pub = grp_clock();
   unsigned long long deadline = 0;
   unsigned spins = 0;
   while (pending && !dead) {
@@ -120,6 +135,7 @@ DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], 
         }
       }
     }
+    if (prof && spins == 0) prof->t_first = grp_clock();
     if (!pending) break;
     // the clock is an SMEM read (it would hold the next LDS wait at lgkmcnt(0)): read it
     // only every 64 polls
@@ -135,6 +151,10 @@ DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], 
         dead = true;
       }
     }
+  }
+  if (prof) {
+    prof->t_end = grp_clock();
+    prof->polls = spins + 1;
   }
   // member order 0..GR-1 on every member (absent members add +0)
 #pragma unroll

@@ -203,6 +203,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
     fidx = fast_index(e2, b2);
   }
   unsigned xepoch = kXgmi ? a.epoch[model] : 0u;
+  // the exchanges' sticky timeout flag, read once per launch with the prologue loads
+  bool xdead = (kXgmi && a.status) ? (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                                   : false;
   unsigned long long xwait = 0;  // exchange-wait ticks of this thread (diagnostic, xgmi_record_wait)
   for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   if (cached) {
@@ -447,7 +450,8 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       // all-reduce (sum) this model's gradient + loss over every rank through
       // the peers' xGMI-mapped receive buffers, inside the step (xgmi_core.h)
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr);
+      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
+                                                1, 0, &xdead);
     }
 
     // advance the sampler / loss-ring position and gather the next step's first
@@ -636,6 +640,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   roll(e2, b2);
   int fidx = fast_index(e2, b2);
   unsigned xepoch = kXgmi ? a.epoch[model] : (GRP ? a.grp_epoch[model] : 0u);  // GRP + xGMI: the xGMI epochs
+  // the exchanges' sticky timeout flag, read once per launch with the prologue loads
+  const int* xst = kXgmi ? a.status : (GRP ? a.grp_status : nullptr);
+  bool xdead = xst ? (__hip_atomic_load(xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
   unsigned long long xwait = 0;
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
@@ -906,7 +913,17 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::losspos()];
     if constexpr (GRP && !kXgmi) {  // the members' partial sums, on chip (grp_core.h)
       xepoch += 1u;
-      lsum = grp_allreduce<NPT, NTH>(gctx, model, P, g, lsum, xepoch, tid);
+      GrpProf gp_;
+      lsum = grp_allreduce<NPT, NTH>(gctx, model, P, g, lsum, xepoch, tid, xdead, PROF ? &gp_ : nullptr);
+      if constexpr (PROF) {  // thread 0: publish issued (16), first poll consumed (17), last granule (31), polls (30)
+        if (tid == 0 && it < 8) {
+          unsigned long long* pr = prof + ((size_t)blockIdx.x * 8 + it) * 32;
+          pr[16] = gp_.t_pub;
+          pr[17] = gp_.t_first;
+          pr[31] = gp_.t_end;
+          pr[30] = gp_.polls;
+        }
+      }
     }
     const float mean_loss = lsum * inv;  // GRP + xGMI: this member's share of the rank's mean
     DTP_STAMP(5);
@@ -914,7 +931,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     if constexpr (kXgmi) {
       xepoch += 1u;
       gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
-                                             GRP ? a.groups : 1, gk);
+                                             GRP ? a.groups : 1, gk, &xdead);
     }
     const int lslot_now = lslot;
     roll(epoch, bi);
@@ -940,7 +957,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
         *(own && pb[k] >= 0 ? &sm.wb[pb[k]] : &sm.sink[1]) = wv;
       }
     }
-    if (tid == (kXgmi ? xgmi_loss_tid<NPT>(P, NTH) : 0) && a.loss_log && lead) {
+    // the thread that holds the summed loss logs it (the loss granule's owner: every other
+    // thread of a split-batch member only has its own member's share)
+    if (tid == ((kXgmi || GRP) ? xgmi_loss_tid<NPT>(P, NTH) : 0) && a.loss_log && lead) {
       const float lg = kXgmi ? gloss * a.hp.grad_scale : mean_loss;
       a.loss_log[(size_t)lslot_now * a.n_models + model] = lg;
     }

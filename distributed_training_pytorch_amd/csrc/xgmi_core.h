@@ -106,8 +106,12 @@ struct XgmiCtx {
 // (its own rank's too: the other local members read it there), so the on-chip partial sums
 // and the cross-GPU sum cost one hop, not two.  Sums run in slot order (rank-major).
 template <int NPT, int NTHREADS = kBlock>
+// dead_io (nullable): the caller's sticky "an exchange timed out" flag, read from the status
+// word ONCE per launch (a status load here would be a vector load behind the publish
+// stores: its vmcnt wait would hold the first poll until every store was acknowledged)
 DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g)[NPT], float loss, unsigned epoch,
-                                   int tid, unsigned long long* waited = nullptr, int GR = 1, int gk = 0) {
+                                   int tid, unsigned long long* waited = nullptr, int GR = 1, int gk = 0,
+                                   bool* dead_io = nullptr) {
   constexpr int GPT = xgmi_gpt<NPT>();
   const int W = a.world * GR, R = a.rank * GR + gk;  // virtual members (slots) and this member's slot
   const int slot = xgmi_slot16(P, NPT);
@@ -145,7 +149,9 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[a.rank]);
   const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
   const unsigned long long deadline = t_pub + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
-  bool dead = a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
+  bool dead = dead_io ? *dead_io
+                      : (a.status ? (__hip_atomic_load(&a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                                  : false);
   float val[kXgmiMaxWorld][GPT + 1][2];
   static_assert(kXgmiMaxWorld * (GPT + 1) <= 64, "pending mask holds every (rank, granule) pair");
   uint64_t pending = 0ull;
@@ -236,6 +242,7 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   }
 #endif
   if (waited) *waited += __builtin_amdgcn_s_memrealtime() - t_pub;
+  if (dead_io) *dead_io = dead;
   // sum in rank order 0..W-1 (bitwise identical on every rank; absent ranks add +0)
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -253,9 +260,9 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
                                    unsigned epoch, int tid, unsigned long long* waited = nullptr, int GR = 1,
-                                   int gk = 0) {
+                                   int gk = 0, bool* dead_io = nullptr) {
   const XgmiCtx c{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
-  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid, waited, GR, gk);
+  return xgmi_allreduce_slots<NPT, NTHREADS>(c, model, P, g, loss, epoch, tid, waited, GR, gk, dead_io);
 }
 
 // the fused step's exchange diagnostics in the status block, for model 0's workgroup:

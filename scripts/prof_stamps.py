@@ -52,6 +52,14 @@ def main():
         if grouped:  # per member of model 0 (blocks 0, 8, 16, ...): exchange = tiles_reduced -> grads_summed
             res.setdefault("members_exchange_cycles", []).append(
                 [[int(st[8 * k, it, 5] - st[8 * k, it, 4]) for it in range(1, 8)] for k in range(tr.groups)])
+            # inside the exchange (thread 0): tiles_reduced -> publish issued -> first poll consumed -> last
+            # granule, polls; and each member's publish time relative to member 0's (skew)
+            res.setdefault("exchange_detail", []).append(
+                [{"to_pub": int(st[8 * k, it, 16] - st[8 * k, it, 4]),
+                  "pub_to_first_poll": int(st[8 * k, it, 17] - st[8 * k, it, 16]),
+                  "pub_to_last": int(st[8 * k, it, 31] - st[8 * k, it, 16]),
+                  "polls": int(st[8 * k, it, 30]),
+                  "pub_skew_vs_m0": int(st[8 * k, it, 16] - st[0, it, 16])} for it in (3, 5) for k in range(tr.groups)])
         rows = []
         for it in range(1, 8):
             s = st[0, it]
