@@ -170,4 +170,130 @@ DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], 
   return lacc;
 }
 
+// The same exchange with the roles split over the waves (the default): wave 0 publishes the
+// member's granules, waves 1.. poll the peers'.  Why: on gfx9 loads and stores share ONE
+// in-order vmcnt, so a wave that polls right after its own publish stores cannot consume its
+// first poll before those write-through stores are acknowledged (measured: one poll after
+// the publish took ~2.9 k cycles, every peer granule already there).  Pollers that never
+// stored see a plain load round trip.  The member's own sums and the peers' values meet in
+// LDS (two barriers):
+//   pub [slot] float2 -- this member's granule payloads (written by their owner threads)
+//   peer[kGrpMax][slot] float2 -- every peer's payloads, in member order
+// Every thread then sums its parameters over the members in order 0..GR-1 (its own value
+// from registers), exactly as grp_allreduce does: the results are the same bits.
+template <int P, int NPT, int NTHREADS>
+DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                                  bool& dead, float2* __restrict__ pub, float2* __restrict__ peer,
+                                  GrpProf* prof = nullptr) {
+  constexpr int GPT = xgmi_gpt<NPT>();
+  constexpr int NPOLL = NTHREADS - kWave;                 // poller lanes (waves 1..)
+  constexpr int slot = grp_slot16(P, NPT);
+  constexpr int nthr = xgmi_nthr(P, NPT);
+  constexpr int ng = nthr * GPT + 1;                      // granules of a member: gradients + the loss
+  constexpr int ltid = xgmi_loss_tid<NPT>(P, NTHREADS);
+  static_assert(NTHREADS > kWave, "one publisher wave and at least one poller wave");
+  const size_t base = (size_t)((int)(epoch & 1u) * c.n_models + model) * c.GR;
+  const bool has_g = tid < nthr;
+  // 1. the owners' payloads into LDS
+#pragma unroll
+  for (int k = 0; k < GPT; ++k)
+    if (has_g) pub[tid * GPT + k] = make_float2(2 * k < NPT ? g[2 * k] : 0.f, 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f);
+  if (tid == ltid) pub[nthr * GPT] = make_float2(loss, 0.f);
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(c.buf);
+  if (tid < kWave) {
+    // 2a. wave 0 publishes every granule of this member once (one 16-byte sc1 store each)
+    for (int q = tid; q < ng; q += kWave) {
+      const float2 v = pub[q];
+      const uint32_t x0 = __float_as_uint(v.x), x1 = __float_as_uint(v.y);
+      const u32x4 qq = {epoch, x0, x1, xgmi_check(epoch, x0, x1)};
+      __builtin_amdgcn_raw_buffer_store_b128(qq, rs, (int)(((base + c.k) * slot + q) * 16), 0, DTP_GRP_ST_AUX);
+    }
+    if (prof) prof->t_pub = grp_clock();
+  } else {
+    // 2b. waves 1.. poll the peers' granules: item i = (peer index i / ng, granule i % ng),
+    // at most MAXI items per lane, all requested at once, only the missing ones re-polled
+    constexpr int MAXI = ((kGrpMax - 1) * ng + NPOLL - 1) / NPOLL;
+    static_assert(MAXI <= 32, "pending mask");
+    const int pl = tid - kWave;
+    const int total = (c.GR - 1) * ng;
+    int off[MAXI], dst[MAXI];
+    uint32_t pending = 0u;
+#pragma unroll
+    for (int j = 0; j < MAXI; ++j) {
+      const int i = pl + j * NPOLL;
+      const int ri = i / ng, q = i - ri * ng;
+      const int r = ri < c.k ? ri : ri + 1;
+      off[j] = (int)(((base + r) * slot + q) * 16);
+      dst[j] = r * slot + q;
+      if (i < total) pending |= 1u << j;
+    }
+    unsigned long long deadline = 0;
+    unsigned spins = 0;
+    if (prof) prof->t_pub = grp_clock();
+    while (pending && !dead) {
+      u32x4 x[MAXI];
+      asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
+#pragma unroll
+      for (int j = 0; j < MAXI; ++j) {
+        x[j] = u32x4{0u, 0u, 0u, 0u};
+        if ((pending >> j) & 1u) x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, DTP_GRP_LD_AUX);
+      }
+#pragma unroll
+      for (int j = 0; j < MAXI; ++j) {
+        if (((pending >> j) & 1u) && x[j].x == epoch && x[j].w == xgmi_check(epoch, x[j].y, x[j].z)) {
+          peer[dst[j]] = make_float2(__uint_as_float(x[j].y), __uint_as_float(x[j].z));
+          pending &= ~(1u << j);
+        }
+      }
+      if (prof && spins == 0) prof->t_first = grp_clock();
+      if (!pending) break;
+      if ((++spins & 63u) == 0u) {
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if (!deadline) {
+          deadline = now + (unsigned long long)(c.timeout_us > 0 ? c.timeout_us : 2000000) * 100ull;
+        } else if (now > deadline) {
+          if (c.status) {
+            atomicExch(&c.status[0], 1);
+            atomicExch(&c.status[1], (int)epoch);
+          }
+          dead = true;
+        }
+      }
+    }
+    if (prof) {
+      prof->t_end = grp_clock();
+      prof->polls = spins + 1;
+    }
+  }
+  __syncthreads();
+  // a poller that timed out told its workgroup through the status word; every thread of the
+  // member takes the flag from there at the next launch (sticky), this step continues
+  // 3. member-order sums (absent members and a timed-out peer's missing values add +0)
+  float own[GPT + 1][2];
+#pragma unroll
+  for (int k = 0; k < GPT; ++k) {
+    own[k][0] = 2 * k < NPT ? g[2 * k] : 0.f;
+    own[k][1] = 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f;
+  }
+  own[GPT][0] = loss;
+  own[GPT][1] = 0.f;
+  float acc[GPT + 1][2];
+#pragma unroll
+  for (int k = 0; k <= GPT; ++k) acc[k][0] = acc[k][1] = 0.f;
+  const int gq0 = has_g ? tid * GPT : 0;
+  for (int r = 0; r < c.GR; ++r) {
+#pragma unroll
+    for (int k = 0; k <= GPT; ++k) {
+      const int q = k < GPT ? gq0 + k : nthr * GPT;
+      const float2 pv = r == c.k ? make_float2(own[k][0], own[k][1]) : peer[r * slot + q];
+      acc[k][0] += pv.x;
+      acc[k][1] += pv.y;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) g[k] = acc[k / 2][k & 1];
+  return acc[GPT][0];
+}
+
 }  // namespace dtp

@@ -37,6 +37,10 @@ constexpr int kAdamTab = 1024;
 
 constexpr int kWaves = kBlock / kWave;
 
+#ifndef DTP_GRP_SPLIT
+#define DTP_GRP_SPLIT 1  // split-batch exchange: publisher / poller waves (grp_allreduce_split); 0: every thread both
+#endif
+
 #ifndef DTP_XWAIT
 #define DTP_XWAIT 1  // 0 (A/B builds only): no exchange-wait diagnostic (bench exchange_wait_us_per_step)
 #endif
@@ -555,7 +559,7 @@ DTP_HD constexpr int lane_area(int l) {
   return (Scal<S>::PACK && (l == 0 || l == S::NL - 1)) ? 0 : (l == S::NL - 1 ? 0 : (l == 0 ? 2 : 1));
 }
 
-template <class S, int L, int NW>
+template <class S, int L, int NW, bool GRP = false>
 struct LaneSmem {
   using C = LaneCfg<S, L>;
   alignas(16) float wb[C::pad4(C::LW)];
@@ -564,6 +568,9 @@ struct LaneSmem {
   alignas(16) float2 adam_tab[kAdamTab];
   alignas(16) float data[kLaneData];
   float sink[4];
+  // split-batch exchange (grp_allreduce_split): this member's payloads, then every member's
+  static constexpr int GSLOT = xgmi_slot16(S::P, (S::P + 64 * NW - 1) / (64 * NW));
+  alignas(16) float2 gx[GRP ? (kGrpMax + 1) * GSLOT : 2];
 };
 
 // NW waves per workgroup (4: one per SIMD; 8: two per SIMD, for batches of 256 / L < B <= 512 / L)
@@ -588,7 +595,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   // GRP with kXgmi: ONE flat exchange over world x groups members (xgmi_core.h)
   static_assert(!CE || S::OUT >= 2, "cross-entropy needs >= 2 classes");
   constexpr int YD = CE ? 1 : S::OUT;  // target floats per sample (a class id for CE)
-  __shared__ __align__(16) LaneSmem<S, L, NW> sm;
+  __shared__ __align__(16) LaneSmem<S, L, NW, GRP && !(MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD)> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = GRP ? (int)(blockIdx.x & 7u) : (int)blockIdx.x;
   const int gk = GRP ? (int)(blockIdx.x >> 3) : 0;  // member of the model's group
@@ -598,6 +605,16 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   const int ws = lane / L;                  // sample slot inside the wave
   const int bk = gk * (NW * C::G) + wave * C::G + ws;  // batch position of this lane's sample
   const GrpCtx gctx{a.grp_buf, a.grp_status, a.groups, gk, a.n_models, a.timeout_us};
+  if constexpr (PROF) {  // placement of this block: XCC id (slot 12) and HW_ID (13) of step 0's row
+    if (tid == 0) {
+      unsigned xcc, hwid;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+      unsigned long long* pr = reinterpret_cast<unsigned long long*>(a.status) + (size_t)blockIdx.x * 8 * 32;
+      pr[12] = xcc;
+      pr[13] = hwid;
+    }
+  }
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
   const float slope = a.hp.slope;
 
@@ -914,9 +931,15 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     if constexpr (GRP && !kXgmi) {  // the members' partial sums, on chip (grp_core.h)
       xepoch += 1u;
       GrpProf gp_;
+#if DTP_GRP_SPLIT
+      lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
+                                              sm.gx + xgmi_slot16(P, NPT), PROF ? &gp_ : nullptr);
+#else
       lsum = grp_allreduce<NPT, NTH>(gctx, model, P, g, lsum, xepoch, tid, xdead, PROF ? &gp_ : nullptr);
-      if constexpr (PROF) {  // thread 0: publish issued (16), first poll consumed (17), last granule (31), polls (30)
-        if (tid == 0 && it < 8) {
+#endif
+      if constexpr (PROF) {  // thread 0 (split: thread 64, a poller): publish issued (16), first poll consumed
+                             // (17), last granule (31), polls (30)
+        if (tid == (DTP_GRP_SPLIT ? 64 : 0) && it < 8) {
           unsigned long long* pr = prof + ((size_t)blockIdx.x * 8 + it) * 32;
           pr[16] = gp_.t_pub;
           pr[17] = gp_.t_first;

@@ -54,6 +54,9 @@ def main():
                 [[int(st[8 * k, it, 5] - st[8 * k, it, 4]) for it in range(1, 8)] for k in range(tr.groups)])
             # inside the exchange (thread 0): tiles_reduced -> publish issued -> first poll consumed -> last
             # granule, polls; and each member's publish time relative to member 0's (skew)
+            # XCC id and HW_ID (CU / SIMD / SE bits) of each member of model 0
+            res.setdefault("placement", []).append([(int(st[8 * k, 0, 12]), hex(int(st[8 * k, 0, 13])))
+                                                    for k in range(tr.groups)])
             res.setdefault("exchange_detail", []).append(
                 [{"to_pub": int(st[8 * k, it, 16] - st[8 * k, it, 4]),
                   "pub_to_first_poll": int(st[8 * k, it, 17] - st[8 * k, it, 16]),

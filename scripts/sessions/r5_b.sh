@@ -2,7 +2,7 @@
 # round 5: split-batch step after the status-load fix: bench A/B, stamps, lanes tests
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r5b
+O=gpurun_out/r5c
 mkdir -p $O
 for i in 1 2; do
 timeout -k 10 150 python bench.py --steps 2000 --warmup 200 >> $O/bench_grp.json 2>> $O/bench.err || exit $?
