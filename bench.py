@@ -39,7 +39,7 @@ from distributed_training_pytorch_amd.data.sampler import SamplerGeometry  # noq
 from distributed_training_pytorch_amd.data.toy_data import ToyData  # noqa: E402
 from distributed_training_pytorch_amd.engine.fused_trainer import EngineConfig, FusedTrainer  # noqa: E402
 from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
-from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC  # noqa: E402
+from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC, MlpSpec  # noqa: E402
 from distributed_training_pytorch_amd.ops.optim import OptimConfig  # noqa: E402
 from distributed_training_pytorch_amd.parallel import comm_util  # noqa: E402
 from distributed_training_pytorch_amd.runtime import bootstrap  # noqa: E402
@@ -74,6 +74,14 @@ def parse():
     ap.add_argument("--cu-mask", choices=["off", "on"], default="off",
                     help="on: run the train kernel on a stream pinned to the first n_models CUs, so its "
                          "code stays in those CUs' instruction cache between launches")
+    ap.add_argument("--optimizer", choices=["adam", "sgd"], default="adam",
+                    help="adam = the reference's Adam(lr=1e-3); sgd = SGD(lr=1e-2, momentum=0.9) (BASELINE north star)")
+    ap.add_argument("--loss", choices=["mse", "ce"], default="mse",
+                    help="mse = the reference's MSELoss (2-10-10-10-10-1); ce = cross-entropy over 4 classes "
+                         "(2-10-10-10-10-4 head, targets bucketed into 4 classes; BASELINE north star)")
+    ap.add_argument("--groups", choices=["auto", "on", "off"], default="auto",
+                    help="split-batch step (csrc/grp_core.h): a rank's batch over batch/64 workgroups per model; "
+                         "auto = the measured policy")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:(local_rank %% device_count), gloo process group "
@@ -212,7 +220,11 @@ def main():
     if world > 1 or a.impl == "stock":  # the stock loop wraps its models in torch DDP even at W=1
         bootstrap.init_process_group(env, "gloo" if (a.share_gpu or dev.type == "cpu") else "nccl", dev)
     n = 512 * world if a.scaling == "weak" else 512
-    ds = ToyData(n=n, seed=a.seed)
+    if a.impl == "stock" and (a.loss != "mse" or a.optimizer != "adam"):
+        raise SystemExit("--impl stock re-enacts the reference loop: MSE + Adam only")
+    ds = ToyData(n=n, seed=a.seed, classes=4 if a.loss == "ce" else 0)
+    spec = MlpSpec(2, 10, 5, 4) if a.loss == "ce" else TOY_SPEC
+    ocfg = OptimConfig(lr=1e-3) if a.optimizer == "adam" else OptimConfig("sgd", 1e-2, momentum=0.9)
 
     if a.impl == "stock":
         from distributed_training_pytorch_amd.baselines.stock import StockLoop
@@ -230,10 +242,14 @@ def main():
         X, Y = ds.device_tensors(dev)
         geom = SamplerGeometry(n=n, world=world, rank=rank, batch=a.batch, seed=a.seed)
         torch.manual_seed(a.seed)
-        init = [ToyModel().flat_params.detach().clone() for _ in range(2)]
+        if a.loss == "ce":  # the 4-class head: torch.nn.Linear's default init of the same layer shapes
+            init = [torch.cat([t.reshape(-1) for lay in [torch.nn.Linear(i, o) for i, o in spec.dims()]
+                               for t in (lay.weight.detach(), lay.bias.detach())]) for _ in range(2)]
+        else:
+            init = [ToyModel().flat_params.detach().clone() for _ in range(2)]
         ecfg = EngineConfig(comm=a.comm, launch=a.launch, steps_per_launch=a.steps_per_launch,
-                            precision=a.precision, sampler=a.sampler)
-        runner = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
+                            precision=a.precision, sampler=a.sampler, groups=a.groups, loss=a.loss)
+        runner = FusedTrainer(spec, 2, X, Y, geom, ocfg, ecfg, init_params=init)
         per_rank_batch = geom.batch_size_at(0)
         train = runner.train
         # the xGMI timeout word is checked right after the timed region (check_comm below)
@@ -345,7 +361,11 @@ def main():
             "dtype": a.precision if a.impl == "native" else "fp32",
             "data": "synthetic (ToyData distribution, seeded; random-init ToyModel weights)",
             "config": {
-                "model": "2x ToyModel MLP 2-10-10-10-10-1 LeakyReLU (X,Y), MSE, Adam lr=1e-3",
+                "model": ("2x ToyModel MLP 2-10-10-10-10-1 LeakyReLU (X,Y), MSE, Adam lr=1e-3"
+                          if (a.loss, a.optimizer) == ("mse", "adam") else
+                          f"2x ToyModel-shaped MLP 2-10-10-10-10-{spec.out_features} LeakyReLU (X,Y), "
+                          f"{'cross-entropy (4 classes)' if a.loss == 'ce' else 'MSE'}, "
+                          f"{'Adam lr=1e-3' if a.optimizer == 'adam' else 'SGD lr=1e-2 momentum=0.9'}"),
                 "global_batch": per_rank_batch * world,
                 "per_rank_batch": per_rank_batch,
                 "seq_len": None,

@@ -54,7 +54,8 @@ struct DtpTrainArgs {
   int adam_tab_len;
   int xbuf_bytes;  // MODE_XGMI_*: bytes of each rank's receive buffer (0: unchecked)
   // split-batch step (grp_core.h): the engine's own exchange buffer, epoch counters and
-  // timeout words; groups = workgroups per model.  Filled by dtp_train_engine_create.
+  // timeout words; groups = workgroups per model.  Filled by dtp_train_engine_create; on
+  // input groups is the caller's request: 0 the measured policy, 1 on, -1 off.
   void* grp_buf;
   unsigned* grp_epoch;
   int* grp_status;

@@ -40,6 +40,17 @@ constexpr int kGrpMax = 8;  // workgroups per model (batch <= 512 at 64 samples 
 #ifndef DTP_GRP_LD_AUX
 #define DTP_GRP_LD_AUX 16  // granule polls: sc1 (L2-served, L1 bypassed)
 #endif
+#ifndef DTP_GRP_SAME_XCD
+// 1: after a launch's first exchange (write-through stores) has shown every member of the
+// model on ONE XCD, publish with plain stores: the lines stay in that XCD's L2 and the
+// members' sc1 polls hit there (a write-through store drops its line from L2, so a poll of
+// it reads beyond L2).  Each member sends its XCC id in the loss granule's spare word, so
+// every member takes the same decision.  Members on different XCDs keep write-through.
+#define DTP_GRP_SAME_XCD 1
+#endif
+#ifndef DTP_GRP_SLEEP0
+#define DTP_GRP_SLEEP0 0  // s_sleep units (64 cycles) before the pollers' first poll (the peers' stores land meanwhile)
+#endif
 
 // granules per (parity, model, member) slot -- the xGMI slot size (xgmi_core.h)
 DTP_HD constexpr int grp_slot16(int P, int npt) { return xgmi_slot16(P, npt); }
@@ -56,6 +67,12 @@ struct GrpProf {
   unsigned long long t_pub, t_first, t_end;
   unsigned polls;
 };
+
+DTP_DEV unsigned grp_xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xFu;
+}
 
 DTP_DEV unsigned long long grp_clock() {
   unsigned long long t;
@@ -181,10 +198,12 @@ DTP_DEV float grp_allreduce(const GrpCtx& c, int model, int P, float (&g)[NPT], 
 //   peer[kGrpMax][slot] float2 -- every peer's payloads, in member order
 // Every thread then sums its parameters over the members in order 0..GR-1 (its own value
 // from registers), exactly as grp_allreduce does: the results are the same bits.
+// xcc: this member's XCC id; plain (in/out, per launch, starts false): publish with plain
+// stores (DTP_GRP_SAME_XCD)
 template <int P, int NPT, int NTHREADS>
 DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
-                                  bool& dead, float2* __restrict__ pub, float2* __restrict__ peer,
-                                  GrpProf* prof = nullptr) {
+                                  bool& dead, float2* __restrict__ pub, float2* __restrict__ peer, unsigned xcc,
+                                  bool& plain, GrpProf* prof = nullptr) {
   constexpr int GPT = xgmi_gpt<NPT>();
   constexpr int NPOLL = NTHREADS - kWave;                 // poller lanes (waves 1..)
   constexpr int slot = grp_slot16(P, NPT);
@@ -198,16 +217,19 @@ DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], f
 #pragma unroll
   for (int k = 0; k < GPT; ++k)
     if (has_g) pub[tid * GPT + k] = make_float2(2 * k < NPT ? g[2 * k] : 0.f, 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f);
-  if (tid == ltid) pub[nthr * GPT] = make_float2(loss, 0.f);
+  if (tid == ltid) pub[nthr * GPT] = make_float2(loss, __uint_as_float(xcc));  // spare word: the XCC id
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(c.buf);
   if (tid < kWave) {
-    // 2a. wave 0 publishes every granule of this member once (one 16-byte sc1 store each)
+    // 2a. wave 0 publishes every granule of this member once (one 16-byte store each:
+    // write-through, or plain once every member is known to share this XCD)
     for (int q = tid; q < ng; q += kWave) {
       const float2 v = pub[q];
       const uint32_t x0 = __float_as_uint(v.x), x1 = __float_as_uint(v.y);
       const u32x4 qq = {epoch, x0, x1, xgmi_check(epoch, x0, x1)};
-      __builtin_amdgcn_raw_buffer_store_b128(qq, rs, (int)(((base + c.k) * slot + q) * 16), 0, DTP_GRP_ST_AUX);
+      const int off = (int)(((base + c.k) * slot + q) * 16);
+      if (DTP_GRP_SAME_XCD && plain) __builtin_amdgcn_raw_buffer_store_b128(qq, rs, off, 0, 0);
+      else __builtin_amdgcn_raw_buffer_store_b128(qq, rs, off, 0, DTP_GRP_ST_AUX);
     }
     if (prof) prof->t_pub = grp_clock();
   } else {
@@ -231,6 +253,7 @@ DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], f
     unsigned long long deadline = 0;
     unsigned spins = 0;
     if (prof) prof->t_pub = grp_clock();
+    if (DTP_GRP_SLEEP0 > 0) __builtin_amdgcn_s_sleep(DTP_GRP_SLEEP0);
     while (pending && !dead) {
       u32x4 x[MAXI];
       asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
@@ -282,6 +305,12 @@ DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], f
 #pragma unroll
   for (int k = 0; k <= GPT; ++k) acc[k][0] = acc[k][1] = 0.f;
   const int gq0 = has_g ? tid * GPT : 0;
+  if (DTP_GRP_SAME_XCD && !plain && !dead) {  // every member on this XCD: plain stores from the next exchange on
+    bool same = true;
+    for (int r = 0; r < c.GR; ++r)
+      if (r != c.k) same = same && __float_as_uint(peer[r * slot + nthr * GPT].y) == xcc;
+    plain = same;
+  }
   for (int r = 0; r < c.GR; ++r) {
 #pragma unroll
     for (int k = 0; k <= GPT; ++k) {

@@ -64,7 +64,7 @@ DTP_DEV void adam_tab_store(float2* __restrict__ lds, int n, int tid, const floa
     if (tid + j * NTH < n) lds[tid + j * NTH] = v[j];
 }
 
-template <class S>
+template <class S, bool XCH = false>
 struct TrainSmem {
   float wb[Scal<S>::LW];  // backward + forward weight blocks (mlp_scalar.h)
   float2 adam_tab[kAdamTab];  // per-step Adam scalars {lr / (1 - b1^t), sqrt(1 - b2^t)}
@@ -76,6 +76,8 @@ struct TrainSmem {
   float data[kDataCache];
   float sink[4];  // target of the optimizer's predicated-off stores (slots past P)
   float lossw[kBlock / kWave];  // bf16 instances: per-wave batch-loss sums (not through a bf16 tile)
+  // xGMI instances: the split exchange's payloads (xgmi_allreduce_split)
+  alignas(16) float2 xg[XCH ? xgmi_split_lds_f2<S::P, S::NPT>() : 2];
 };
 
 // One lane's sample of a step: input, target (class index for CE) and validity.
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   using SC = Scal<S>;
   constexpr int NL = S::NL, P = S::P, NT = SC::NT, NPT = S::NPT;
   static_assert(NT * SC::TSZ <= 2 * 2 * kStgArr, "a wave's reduction tiles must fit in its staging area");
-  __shared__ __align__(16) TrainSmem<S> sm;
+  __shared__ __align__(16) TrainSmem<S, DTP_XGMI_SPLIT && (MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD)> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = blockIdx.x;
   constexpr bool kUpdate = MODE != DTP_MODE_GRAD;
@@ -454,8 +456,14 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
       // all-reduce (sum) this model's gradient + loss over every rank through
       // the peers' xGMI-mapped receive buffers, inside the step (xgmi_core.h)
       xepoch += 1u;
+#if DTP_XGMI_SPLIT
+      const XgmiCtx xc{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
+      gloss = xgmi_allreduce_split<P, NPT, kBlock>(xc, model, g, mean_loss, xepoch, tid, sm.xg,
+                                                   sm.xg + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? &xwait : nullptr);
+#else
       gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
                                                 1, 0, &xdead);
+#endif
     }
 
     // advance the sampler / loss-ring position and gather the next step's first
@@ -595,7 +603,10 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   // GRP with kXgmi: ONE flat exchange over world x groups members (xgmi_core.h)
   static_assert(!CE || S::OUT >= 2, "cross-entropy needs >= 2 classes");
   constexpr int YD = CE ? 1 : S::OUT;  // target floats per sample (a class id for CE)
-  __shared__ __align__(16) LaneSmem<S, L, NW, GRP && !(MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD)> sm;
+  // the split exchanges' LDS: the split-batch step, and the xGMI instances of 4 waves (the
+  // 8-wave ones keep the single-role exchange: their LDS is full)
+  constexpr bool kXsplit = DTP_XGMI_SPLIT && NW == 4 && (MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD);
+  __shared__ __align__(16) LaneSmem<S, L, NW, GRP || kXsplit> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = GRP ? (int)(blockIdx.x & 7u) : (int)blockIdx.x;
   const int gk = GRP ? (int)(blockIdx.x >> 3) : 0;  // member of the model's group
@@ -660,6 +671,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   // the exchanges' sticky timeout flag, read once per launch with the prologue loads
   const int* xst = kXgmi ? a.status : (GRP ? a.grp_status : nullptr);
   bool xdead = xst ? (__hip_atomic_load(xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
+  const unsigned xcc = GRP ? grp_xcc_id() : 0u;  // split-batch exchange: plain stores once every member shares it
+  bool gplain = false;
   unsigned long long xwait = 0;
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
@@ -933,7 +946,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       GrpProf gp_;
 #if DTP_GRP_SPLIT
       lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
-                                              sm.gx + xgmi_slot16(P, NPT), PROF ? &gp_ : nullptr);
+                                              sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr);
 #else
       lsum = grp_allreduce<NPT, NTH>(gctx, model, P, g, lsum, xepoch, tid, xdead, PROF ? &gp_ : nullptr);
 #endif
@@ -953,8 +966,15 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     float gloss = mean_loss;
     if constexpr (kXgmi) {
       xepoch += 1u;
-      gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
-                                             GRP ? a.groups : 1, gk, &xdead);
+      if constexpr (kXsplit) {
+        const XgmiCtx xc{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
+        gloss = xgmi_allreduce_split<P, NPT, NTH>(xc, model, g, mean_loss, xepoch, tid, sm.gx,
+                                                  sm.gx + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? &xwait : nullptr,
+                                                  GRP ? a.groups : 1, gk);
+      } else {
+        gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
+                                               GRP ? a.groups : 1, gk, &xdead);
+      }
     }
     const int lslot_now = lslot;
     roll(epoch, bi);
@@ -1206,20 +1226,33 @@ int xgmi_max_slot16(int P) {
 // Split-batch step (engine launches only: it owns the exchange buffer): a per-rank batch
 // above 64 on one rank runs on ceil(batch / 64) workgroups per model, each the 4-lanes step
 // on 64 samples, their gradients summed on chip.  DTP_GROUPS=1 turns it off (A/B runs).
-int pick_groups(const DtpTrainArgs& a, int in, int out, bool allow) {
-  static const int env = [] {
+// DTP_GROUPS: unset = the measured policy below, "on" = wherever an instance exists,
+// "off" / "0" / "1" = never (A/B runs)
+int pick_groups(const DtpTrainArgs& a, int in, int out, bool allow, bool fast1) {
+  static const int env = [] {  // -1 policy, 0 off, 1 on
     const char* e = getenv("DTP_GROUPS");
-    return e ? atoi(e) : 0;
+    if (!e) return -1;
+    return strcmp(e, "on") == 0 ? 1 : 0;
   }();
   static const bool forced_lanes = getenv("DTP_LANES") != nullptr;  // a forced lanes instance runs as asked
-  if (!allow || env == 1 || forced_lanes || a.n_models > 8) return 1;
+  // the caller's request (DtpTrainArgs.groups before the engine fills it in): 0 policy,
+  // 1 on, -1 off; the environment wins (A/B runs)
+  const int want = env >= 0 ? env : (a.groups > 0 ? 1 : (a.groups < 0 ? 0 : -1));
+  if (!allow || want == 0 || forced_lanes || a.n_models > 8) return 1;
   if (a.smp.n * (in + out) > dtp::kLaneData) return 1;
   const int b = min(a.smp.batch, a.smp.num_samples);
   if (b <= 64) return 1;
   const int gr = (b + 63) / 64;
   // several ranks: one flat exchange over world x groups virtual members (xgmi_core.h)
   const int cap = a.smp.world == 1 ? dtp::kGrpMax : dtp::kXgmiMaxWorld / a.smp.world;
-  return gr <= cap ? gr : 1;
+  if (gr > cap) return 1;
+  if (want == 1) return gr;
+  // the policy (docs/perf_notes.md "Round 5: the split-batch step"): one rank keeps the
+  // one-lane FAST step -- an on-chip hand-off costs ~1 k cycles per memory round trip, 2-3 k
+  // per exchange, about what the split saves; with several ranks the exchange is paid
+  // anyway, so the split's shorter compute shows; and where there is no FAST one-lane
+  // instance (SGD, cross-entropy) the split beats the generic one: on for 4 members per model
+  return ((a.smp.world > 1 || !fast1) && gr >= 4) ? gr : 1;
 }
 
 LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {
@@ -1254,7 +1287,7 @@ TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int ou
   const bool ce = a.loss == DTP_LOSS_CE;
   LanePick lp = pick_lanes(a, in, out, base);
   if (base) {
-    const int gr = pick_groups(a, in, out, allow_groups);
+    const int gr = pick_groups(a, in, out, allow_groups, fast);
     if (gr > 1) {
       if (TrainLaunchFn f = grp_inst(in, h, nl, out, mode, ce, a.bf16)) {
         if (pick) *pick = LanePick{4, 4, gr};

@@ -257,6 +257,143 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   return lacc;
 }
 
+#ifndef DTP_XGMI_SPLIT
+// 1: the fused steps' xGMI exchange with publisher / poller waves (xgmi_allreduce_split).
+// Off: in the one-GPU multi-rank rehearsal it measured slower (W = 2 / 4 / 8: 5.65 / 6.58 /
+// 9.00 vs 5.60 / 6.40 / 8.04 us/step, profiles/r5_exchange/), the single publisher wave
+// issuing (W - 1) x 187 stores at W = 8.  The on-chip split-batch exchange keeps its split
+// (grp_core.h), where it measured faster.
+#define DTP_XGMI_SPLIT 0
+#endif
+#ifndef DTP_XGMI_PUB_WAVES
+#define DTP_XGMI_PUB_WAVES 1  // waves that publish (the rest poll)
+#endif
+
+// LDS of the split exchange: this member's payloads [slot], then every virtual member's [8][slot]
+template <int P, int NPT>
+DTP_HD constexpr int xgmi_split_lds_f2() {
+  return (1 + kXgmiMaxWorld) * xgmi_slot16(P, NPT);
+}
+
+// The same all-reduce with the roles split over the waves, as grp_allreduce_split
+// (grp_core.h): gfx9 counts loads and stores in ONE in-order vmcnt, so a thread that polls
+// right after its own publish stores cannot consume its first poll before those stores --
+// posted xGMI writes to every peer -- are acknowledged.  Here the first DTP_XGMI_PUB_WAVES
+// waves publish every granule of this (virtual) member to every rank that reads it, the
+// other waves poll, and the payloads meet in LDS (two barriers).  Sums run in slot order, so
+// the result is bitwise that of xgmi_allreduce_slots.  waited: the polling thread's wait
+// (publish -> last granule accepted, s_memrealtime ticks), for the bench diagnostic.
+template <int P, int NPT, int NTHREADS>
+DTP_DEV float xgmi_allreduce_split(const XgmiCtx& a, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                                   float2* __restrict__ pub, float2* __restrict__ peer, bool& dead,
+                                   unsigned long long* waited = nullptr, int GR = 1, int gk = 0) {
+  constexpr int GPT = xgmi_gpt<NPT>();
+  constexpr int NPUB = kWave * DTP_XGMI_PUB_WAVES;          // publisher lanes
+  constexpr int NPOLL = NTHREADS - NPUB;                     // poller lanes
+  static_assert(NPOLL >= kWave, "at least one poller wave");
+  constexpr int slot = xgmi_slot16(P, NPT);
+  constexpr int nthr = xgmi_nthr(P, NPT);
+  constexpr int ng = nthr * GPT + 1;                         // granules of a member: gradients + the loss
+  constexpr int ltid = xgmi_loss_tid<NPT>(P, NTHREADS);
+  const int V = a.world * GR, R = a.rank * GR + gk;          // virtual members (slots), this member's slot
+  const size_t base = (size_t)((int)(epoch & 1u) * a.n_models + model) * V;
+  const bool has_g = tid < nthr;
+#pragma unroll
+  for (int k = 0; k < GPT; ++k)
+    if (has_g) pub[tid * GPT + k] = make_float2(2 * k < NPT ? g[2 * k] : 0.f, 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f);
+  if (tid == ltid) pub[nthr * GPT] = make_float2(loss, 0.f);
+  __syncthreads();
+  if (tid < NPUB) {
+    // publish: every granule once into every rank's buffer that has a reader of this slot
+    // (this rank's own buffer too when other members of the rank read it)
+    for (int r = 0; r < a.world; ++r) {
+      if (r == a.rank && GR == 1) continue;
+      const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(a.peers[r]);
+      for (int q = tid; q < ng; q += NPUB) {
+        const float2 v = pub[q];
+        const uint32_t x0 = __float_as_uint(v.x), x1 = __float_as_uint(v.y);
+        const u32x4 qq = {epoch, x0, x1, xgmi_check(epoch, x0, x1)};
+        __builtin_amdgcn_raw_buffer_store_b128(qq, rs, (int)(((base + R) * slot + q) * 16), 0, kSysCoherent);
+      }
+    }
+  } else {
+    // poll the other V - 1 slots of the local buffer: item i = (slot index i / ng, granule
+    // i % ng), at most MAXI per lane, all requested at once, only the missing ones re-polled
+    constexpr int MAXI = ((kXgmiMaxWorld - 1) * ng + NPOLL - 1) / NPOLL;
+    static_assert(MAXI <= 32, "pending mask");
+    const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[a.rank]);
+    const int pl = tid - NPUB;
+    const int total = (V - 1) * ng;
+    int off[MAXI], dst[MAXI];
+    uint32_t pending = 0u;
+#pragma unroll
+    for (int j = 0; j < MAXI; ++j) {
+      const int i = pl + j * NPOLL;
+      const int vi = i / ng, q = i - vi * ng;
+      const int v = vi < R ? vi : vi + 1;
+      off[j] = (int)(((base + v) * slot + q) * 16);
+      dst[j] = v * slot + q;
+      if (i < total) pending |= 1u << j;
+    }
+    const unsigned long long t_pub = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long deadline = t_pub + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
+    unsigned spins = 0;
+    while (pending && !dead) {
+      u32x4 x[MAXI];
+      asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
+#pragma unroll
+      for (int j = 0; j < MAXI; ++j) {
+        x[j] = u32x4{0u, 0u, 0u, 0u};
+        if ((pending >> j) & 1u) x[j] = __builtin_amdgcn_raw_buffer_load_b128(ms, off[j], 0, kSysCoherent);
+      }
+#pragma unroll
+      for (int j = 0; j < MAXI; ++j) {
+        if (((pending >> j) & 1u) && x[j].x == epoch && x[j].w == xgmi_check(epoch, x[j].y, x[j].z)) {
+          peer[dst[j]] = make_float2(__uint_as_float(x[j].y), __uint_as_float(x[j].z));
+          pending &= ~(1u << j);
+        }
+      }
+      if (!pending) break;
+      if ((++spins & 15u) == 0u && __builtin_amdgcn_s_memrealtime() > deadline) {
+        if (a.status) {
+          atomicExch(&a.status[0], 1);
+          atomicExch(&a.status[1], (int)epoch);
+        }
+        dead = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (waited) *waited += __builtin_amdgcn_s_memrealtime() - t_pub;
+  }
+  __syncthreads();
+  // slot-order sums (absent slots add nothing; a timed-out peer's stale values are flagged)
+  float own[GPT + 1][2];
+#pragma unroll
+  for (int k = 0; k < GPT; ++k) {
+    own[k][0] = 2 * k < NPT ? g[2 * k] : 0.f;
+    own[k][1] = 2 * k + 1 < NPT ? g[2 * k + 1] : 0.f;
+  }
+  own[GPT][0] = loss;
+  own[GPT][1] = 0.f;
+  float acc[GPT + 1][2];
+#pragma unroll
+  for (int k = 0; k <= GPT; ++k) acc[k][0] = acc[k][1] = 0.f;
+  const int gq0 = has_g ? tid * GPT : 0;
+  for (int v = 0; v < V; ++v) {
+#pragma unroll
+    for (int k = 0; k <= GPT; ++k) {
+      const int q = k < GPT ? gq0 + k : nthr * GPT;
+      const float2 pv = v == R ? make_float2(own[k][0], own[k][1]) : peer[v * slot + q];
+      acc[k][0] += pv.x;
+      acc[k][1] += pv.y;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) g[k] = acc[k / 2][k & 1];
+  return acc[GPT][0];
+}
+
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
                                    unsigned epoch, int tid, unsigned long long* waited = nullptr, int GR = 1,

@@ -50,6 +50,9 @@ class EngineConfig:
     xgmi_selftest: bool = True        # validate the xGMI exchange against a host all-reduce, else fall back
     rccl_graph: bool = True      # capture grad->all_reduce->optimizer into a hipGraph
     precision: str = "fp32"      # fp32 | bf16 (bf16 matmul operands, fp32 accumulation / master weights / Adam)
+    # split-batch step (csrc/grp_core.h: a rank's batch over batch/64 workgroups per model):
+    # auto = the measured policy (on for 4 members per model with several ranks), on, off
+    groups: str = "auto"
 
 
 class FusedTrainer:
@@ -307,6 +310,9 @@ class FusedTrainer:
             a.adam_tab, a.adam_tab_len = nat.ptr(tab), tab.shape[0]
         if xg is not None:
             a.xbuf_bytes = xg.nbytes
+        if self.cfg.groups not in ("auto", "on", "off"):
+            raise ValueError(f"groups {self.cfg.groups!r}: auto, on or off")
+        a.groups = {"auto": 0, "on": 1, "off": -1}[self.cfg.groups]
         return a
 
     def _update_mode(self) -> int:

@@ -88,10 +88,11 @@ def test_bench_strong_scaling_share_gpu(world):
     assert rec["config"]["dataset_samples"] == 512
     assert rec["config"]["global_batch"] == 512
     assert rec["config"]["per_rank_batch"] == 512 // world
-    # per-rank batch 256 / 128 / 64: the 4-lanes step on 4 / 2 / 1 workgroups per model (the
-    # split-batch members join the xGMI exchange as world x groups virtual members)
-    assert rec["config"]["lanes_per_sample"] == 4, rec["config"]
-    assert rec["config"]["workgroups_per_model"] == {2: 4, 4: 2, 8: 1}[world], rec["config"]
+    # per-rank batch 256 / 128 / 64: the 4-lanes step on 4 workgroups per model (the
+    # split-batch members join the xGMI exchange as world x groups virtual members), the
+    # 2-lanes step, the 4-lanes step
+    assert (rec["config"]["lanes_per_sample"], rec["config"]["workgroups_per_model"]) == \
+        {2: (4, 4), 4: (2, 1), 8: (4, 1)}[world], rec["config"]
     # the multi-GPU diagnostics of the line: no fallback, exchange wait and compute split
     assert rec["comm_fallback_reason"] is None
     assert len(rec["exchange_wait_us_per_step_by_rank"]) == world

@@ -121,7 +121,7 @@ def test_bf16_lanes_and_split_batch_steps_match_rounding_model(batch, lanes, gro
     g = torch.Generator().manual_seed(9)
     init = [torch.randn(TOY_SPEC.P, generator=g) * 0.4 for _ in range(2)]
     ocfg = OptimConfig(lr=1e-2)
-    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=5, precision="bf16"),
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=5, precision="bf16", groups="on"),
                       init_params=[p.to(DEV) for p in init])
     assert (tr.lanes, tr.groups) == (lanes, groups)
     steps = 10

@@ -38,7 +38,7 @@ def test_lanes_selected_by_batch_and_match_torch(batch, lanes, groups):
     geom = SamplerGeometry(n=512, batch=batch, seed=3)
     init = _init(TOY_SPEC, batch)
     ocfg = OptimConfig(lr=1e-2)
-    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=7), init_params=init)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=7, groups="on"), init_params=init)
     assert (tr.lanes, tr.groups) == (lanes, groups)
     steps = 2 * geom.steps_per_epoch + 3
     tr.train(steps)
@@ -84,11 +84,11 @@ def test_lanes_bitwise_across_launch_modes(batch):
     geom = SamplerGeometry(n=512, batch=batch, seed=1)
     init = _init(TOY_SPEC, 40)
     res = {}
-    for name, ecfg, steps in [("long", EngineConfig(steps_per_launch=1100), 1100),
-                              ("short", EngineConfig(steps_per_launch=100), 1100),
-                              ("one", EngineConfig(steps_per_launch=1100), 30),
-                              ("eager", EngineConfig(launch="eager"), 30),
-                              ("graph", EngineConfig(launch="graph", steps_per_launch=8), 30)]:
+    for name, ecfg, steps in [("long", EngineConfig(steps_per_launch=1100, groups="on"), 1100),
+                              ("short", EngineConfig(steps_per_launch=100, groups="on"), 1100),
+                              ("one", EngineConfig(steps_per_launch=1100, groups="on"), 30),
+                              ("eager", EngineConfig(launch="eager", groups="on"), 30),
+                              ("graph", EngineConfig(launch="graph", steps_per_launch=8, groups="on"), 30)]:
         tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-3), ecfg, init_params=init)
         assert (tr.lanes, tr.groups) == (4, batch // 64)
         tr.train(steps)
@@ -114,7 +114,7 @@ X, Y = ToyData(n=512, seed=8).device_tensors(dev)
 g = torch.Generator().manual_seed(0)
 init = [(torch.randn(TOY_SPEC.P, generator=g) * 0.4).to(dev) for _ in range(2)]
 tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch={batch}, seed=4), OptimConfig(lr=1e-2),
-                  EngineConfig(steps_per_launch=9), init_params=init)
+                  EngineConfig(steps_per_launch=9, groups={groups!r}), init_params=init)
 lanes = tr.lanes
 tr.train(40)
 tr.synchronize()
@@ -130,7 +130,7 @@ def test_lanes_agree_with_one_lane_kernel(tmp_path):
     for flag in ("1", "2", "4"):
         out = str(tmp_path / f"l{flag}.pt")
         env = dict(os.environ, DTP_LANES=flag)
-        r = subprocess.run([sys.executable, "-c", _FORCE_SCRIPT.format(root=ROOT, batch=64, out=out)], env=env,
+        r = subprocess.run([sys.executable, "-c", _FORCE_SCRIPT.format(root=ROOT, batch=64, out=out, groups="auto")], env=env,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         outs[flag] = torch.load(out, weights_only=True)
@@ -142,22 +142,21 @@ def test_lanes_agree_with_one_lane_kernel(tmp_path):
 
 @pytest.mark.parametrize("batch", [256, 128])
 def test_split_batch_step_agrees_with_single_workgroup(batch, tmp_path):
-    """DTP_GROUPS=1 turns the split-batch step off: the same run on one workgroup per
-    model (the one-lane step at 256, the 2-lanes step at 128) agrees with it to float
-    reassociation."""
+    """The split-batch step (groups="on") and the one-workgroup step (groups="off": the
+    one-lane step at 256, the 2-lanes step at 128) run the same training to float
+    reassociation; the default policy at one rank is the one-workgroup step."""
     outs = {}
-    for flag in ("1", "auto"):
+    for flag in ("off", "on", "auto"):
         out = str(tmp_path / f"g{flag}.pt")
         env = {k: v for k, v in os.environ.items() if k not in ("DTP_LANES", "DTP_GROUPS")}
-        if flag == "1":
-            env["DTP_GROUPS"] = "1"
-        r = subprocess.run([sys.executable, "-c", _FORCE_SCRIPT.format(root=ROOT, batch=batch, out=out)],
+        r = subprocess.run([sys.executable, "-c", _FORCE_SCRIPT.format(root=ROOT, batch=batch, out=out, groups=flag)],
                            env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         outs[flag] = torch.load(out, weights_only=True)
-    assert outs["1"]["lanes"] == (1 if batch == 256 else 2) and outs["auto"]["lanes"] == 4
-    torch.testing.assert_close(outs["auto"]["l"], outs["1"]["l"], rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(outs["auto"]["p"], outs["1"]["p"], rtol=1e-4, atol=1e-6)
+    assert outs["off"]["lanes"] == (1 if batch == 256 else 2) and outs["on"]["lanes"] == 4
+    assert torch.equal(outs["auto"]["p"], outs["off"]["p"])
+    torch.testing.assert_close(outs["on"]["l"], outs["off"]["l"], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(outs["on"]["p"], outs["off"]["p"], rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("batch", [256, 64])

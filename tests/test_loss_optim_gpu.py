@@ -147,7 +147,7 @@ def test_lanes_and_split_batch_loss_optim(batch, groups, loss, optim):
     ds = _data(loss)
     X, Y = ds.device_tensors(DEV)
     geom = SamplerGeometry(n=512, batch=batch, seed=11)
-    tr = FusedTrainer(spec, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=4, loss=loss),
+    tr = FusedTrainer(spec, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=4, loss=loss, groups="on"),
                       init_params=[p.to(DEV) for p in _init(spec, 100)])
     assert (tr.lanes, tr.groups) == (4, groups)
     steps = 11

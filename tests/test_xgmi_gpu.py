@@ -19,14 +19,15 @@ pytestmark = pytest.mark.gpu
 STEPS = 9
 
 
-def _gpu_rank(rank, world, comm, steps, launch, sampler="torch"):
+def _gpu_rank(rank, world, comm, steps, launch, sampler="torch", groups="auto"):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     ds = ToyData(n=512, seed=1)
     X, Y = ds.device_tensors(dev)
     geom = SamplerGeometry(n=512, world=world, rank=rank, batch=128, seed=3)
     tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, OptimConfig(lr=1e-2),
-                      EngineConfig(comm=comm, launch=launch, steps_per_launch=4, sampler=sampler), init_params=_init(100 + rank))
+                      EngineConfig(comm=comm, launch=launch, steps_per_launch=4, sampler=sampler, groups=groups),
+                      init_params=_init(100 + rank))
     tr.train(steps)
     tr.synchronize()
     out = (tr.params.cpu(), tr.losses(0, steps), tr.comm)
@@ -41,6 +42,20 @@ def test_two_ranks_one_gpu(comm, launch):
     for r in range(2):
         p, l, used = res[r]
         assert used == comm, f"rank {r} fell back to {used}"
+        torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=2e-5)
+        torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
+    assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
+
+
+@pytest.mark.parametrize("launch", ["persistent", "graph"])
+def test_two_ranks_split_batch_flat_exchange(launch):
+    """groups="on" at per-rank batch 128: each rank runs the step on 2 workgroups per model
+    and the 2 x 2 members all-reduce in ONE flat xGMI exchange (4 virtual members)."""
+    res = run_ranks(_gpu_rank, 2, ("xgmi", STEPS, launch, "torch", "on"), timeout=300)
+    ref_p, ref_l = _reference(2, STEPS)
+    for r in range(2):
+        p, l, used = res[r]
+        assert used == "xgmi", f"rank {r} fell back to {used}"
         torch.testing.assert_close(p, ref_p, rtol=1e-4, atol=2e-5)
         torch.testing.assert_close(l, ref_l, rtol=1e-4, atol=1e-5)
     assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
