@@ -631,3 +631,5 @@ class FusedLayerSplit:
                 self.lib.dtp_free(ctypes.c_void_p(ptr))
         self._owned = []
         self._link_tensors = []
+        for ring in getattr(self, "rings", {}).values():
+            ring.close()  # its generator thread may be inside the native randperm
