@@ -326,10 +326,16 @@ def main():
         # exchange's wait (publish -> last peer granule, per rank) and the rest of the step
         diag["comm_fallback_reason"] = runner.comm_fallback_reason
         if xstats:
-            w_us, n_ex = runner.exchange_stats()
-            waits = comm_util.all_gather_scalar(w_us / max(1, n_ex))
+            st = runner.exchange_stats_full()
+            n_ex = max(1, st["exchanges"])
+            waits = comm_util.all_gather_scalar(st["wait_us"] / n_ex)
+            pubs = comm_util.all_gather_scalar(st["publish_us"] / n_ex)
             diag["exchange_wait_us_per_step"] = max(waits)
             diag["exchange_wait_us_per_step_by_rank"] = [round(v, 3) for v in waits]
+            # the step three ways: publishing the granules (first -> last store issued),
+            # waiting for the peers' granules, and the rest of the step
+            diag["publish_us_per_step"] = max(pubs)
+            diag["step_rest_us_per_step"] = 1e3 * ms_per_step - max(waits) - max(pubs)
             diag["compute_us_per_step"] = 1e3 * ms_per_step - max(waits)
 
     final_loss = None

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
   // the exchanges' sticky timeout flag, read once per launch with the prologue loads
   bool xdead = (kXgmi && a.status) ? (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
                                    : false;
-  unsigned long long xwait = 0;  // exchange-wait ticks of this thread (diagnostic, xgmi_record_wait)
+  unsigned long long xwait[2] = {0ull, 0ull};  // exchange-wait / publish ticks of this thread (xgmi_record_wait)
   for (int e = tid; e < SC::LW; e += kBlock) sm.wb[e] = 0.f;
   if (cached) {
     for (int e = tid; e < smp.n * S::IN; e += kBlock) sm.data[e] = a.X[e];
@@ -459,9 +459,9 @@ __global__ __launch_bounds__(kBlock) DTP_TRAIN_ATTR void mlp_train_kernel(DtpTra
 #if DTP_XGMI_SPLIT
       const XgmiCtx xc{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
       gloss = xgmi_allreduce_split<P, NPT, kBlock>(xc, model, g, mean_loss, xepoch, tid, sm.xg,
-                                                   sm.xg + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? &xwait : nullptr);
+                                                   sm.xg + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? xwait : nullptr);
 #else
-      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
+      gloss = xgmi_allreduce_model<NPT, kBlock>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? xwait : nullptr,
                                                 1, 0, &xdead);
 #endif
     }
@@ -673,7 +673,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   bool xdead = xst ? (__hip_atomic_load(xst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) : false;
   const unsigned xcc = GRP ? grp_xcc_id() : 0u;  // split-batch exchange: plain stores once every member shares it
   bool gplain = false;
-  unsigned long long xwait = 0;
+  unsigned long long xwait[2] = {0ull, 0ull};
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
   for (int e = tid; e < smp.n * YD; e += NTH) sm.data[smp.n * S::IN + e] = a.Y[e];
@@ -969,10 +969,10 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       if constexpr (kXsplit) {
         const XgmiCtx xc{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
         gloss = xgmi_allreduce_split<P, NPT, NTH>(xc, model, g, mean_loss, xepoch, tid, sm.gx,
-                                                  sm.gx + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? &xwait : nullptr,
+                                                  sm.gx + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? xwait : nullptr,
                                                   GRP ? a.groups : 1, gk);
       } else {
-        gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? &xwait : nullptr,
+        gloss = xgmi_allreduce_model<NPT, NTH>(a, model, P, g, mean_loss, xepoch, tid, DTP_XWAIT ? xwait : nullptr,
                                                GRP ? a.groups : 1, gk, &xdead);
       }
     }

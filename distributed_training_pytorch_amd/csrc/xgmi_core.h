@@ -97,9 +97,10 @@ struct XgmiCtx {
   int world, rank, n_models, timeout_us;
 };
 
-// waited (nullable): += s_memrealtime ticks (100 MHz) from this thread's last publish
-// store to its last granule accepted -- the exchange-wait diagnostic of the bench
-// (status words [4..8), written back once per launch by the caller)
+// waited (nullable, 2 words): [0] += s_memrealtime ticks (100 MHz) from this thread's last
+// publish store issued to its last granule accepted, [1] += ticks from its first to its last
+// publish store issued -- the exchange-wait and publish diagnostics of the bench (status
+// words [4..14), written back once per launch by the caller)
 // GR > 1 (the split-batch step, grp_core.h): every rank runs the step on GR workgroups per
 // model, and the exchange is ONE flat all-reduce over V = W GR virtual members -- member k
 // of rank R is slot R GR + k of every receive buffer, stored once into each rank's buffer
@@ -131,6 +132,7 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
   v[GPT][1] = 0.f;
   auto gidx = [&](int k) { return k < GPT ? tid * GPT + k : nthr * GPT; };  // granule index in a slot
   auto mine_k = [&](int k) { return k < GPT ? has_g : has_l; };
+  const unsigned long long t_pub0 = waited ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // publish to every rank that has a reader of this slot (posted xGMI writes; our own
   // contribution stays in registers)
   for (int r = 0; r < a.world; ++r) {
@@ -241,7 +243,10 @@ DTP_DEV float xgmi_allreduce_slots(const XgmiCtx& a, int model, int P, float (&g
     __builtin_amdgcn_s_sleep(1);
   }
 #endif
-  if (waited) *waited += __builtin_amdgcn_s_memrealtime() - t_pub;
+  if (waited) {
+    waited[0] += __builtin_amdgcn_s_memrealtime() - t_pub;
+    waited[1] += t_pub - t_pub0;
+  }
   if (dead_io) *dead_io = dead;
   // sum in rank order 0..W-1 (bitwise identical on every rank; absent ranks add +0)
 #pragma unroll
@@ -364,7 +369,7 @@ DTP_DEV float xgmi_allreduce_split(const XgmiCtx& a, int model, float (&g)[NPT],
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (waited) *waited += __builtin_amdgcn_s_memrealtime() - t_pub;
+    if (waited) waited[0] += __builtin_amdgcn_s_memrealtime() - t_pub;
   }
   __syncthreads();
   // slot-order sums (absent slots add nothing; a timed-out peer's stale values are flagged)
@@ -405,17 +410,21 @@ DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, floa
 // the fused step's exchange diagnostics in the status block, for model 0's workgroup:
 // [4..6) u64 += the launch's exchange-wait ticks of its SLOWEST thread (the step cannot
 // pass its closing barrier before that thread has every peer granule), [6..8) u64 +=
-// the launch's exchanges; [8..10) is the per-launch max scratch.  Accumulated over
-// launches; the host zeroes them around a timed region.  Called by EVERY thread of the
-// workgroup at the end of the launch (contains a barrier).
-DTP_DEV void xgmi_record_wait(int* status, unsigned long long ticks, unsigned long long n, int tid) {
+// the launch's exchanges; [8..10) is the per-launch max scratch; [10..12) u64 += the
+// launch's publish ticks of its slowest publisher, [12..14) its max scratch.  Accumulated
+// over launches; the host zeroes them around a timed region.  Called by EVERY thread of
+// the workgroup at the end of the launch (contains a barrier).
+DTP_DEV void xgmi_record_wait(int* status, const unsigned long long (&ticks)[2], unsigned long long n, int tid) {
   unsigned long long* w = reinterpret_cast<unsigned long long*>(status + 4);
-  atomicMax(w + 2, ticks);
+  atomicMax(w + 2, ticks[0]);
+  atomicMax(w + 4, ticks[1]);
   __syncthreads();  // every thread's max has landed (device-coherent atomics, then the barrier)
   if (tid == 0) {
     const unsigned long long m = atomicExch(w + 2, 0ull);
+    const unsigned long long mp = atomicExch(w + 4, 0ull);
     atomicAdd(w, m);
     atomicAdd(w + 1, n);
+    atomicAdd(w + 3, mp);
   }
 }
 

@@ -515,19 +515,28 @@ class FusedTrainer:
         return buf[:n * P].view(n, P), buf[n * P:n * P + n]
 
     def exchange_stats_reset(self) -> None:
-        """Zero the in-kernel exchange's wait counters (status words [4..10), stream-ordered)."""
+        """Zero the in-kernel exchange's wait / publish counters (status words [4..14),
+        stream-ordered)."""
         if self._xgmi is not None:
-            self._xgmi.status[4:10].zero_()
+            self._xgmi.status[4:14].zero_()
 
     def exchange_stats(self) -> tuple[float, int] | None:
         """(microseconds model 0's slowest thread spent between publishing its gradient
         granules and accepting its last peer granule, summed over the launches since the
         last reset; number of exchanges) -- None without the in-kernel xGMI exchange.
         Syncs."""
+        st = self.exchange_stats_full()
+        return None if st is None else (st["wait_us"], st["exchanges"])
+
+    def exchange_stats_full(self) -> dict | None:
+        """The exchange diagnostics since the last reset: ``wait_us`` (as exchange_stats),
+        ``publish_us`` (the slowest publisher's first -> last granule store issued, summed
+        over launches) and ``exchanges``.  None without the in-kernel xGMI exchange.  Syncs."""
         if self._xgmi is None:
             return None
-        w = self._xgmi.status[4:8].cpu().view(torch.int64).tolist()
-        return w[0] / 100.0, int(w[1])  # s_memrealtime runs at 100 MHz
+        w = self._xgmi.status[4:14].cpu().view(torch.int64).tolist()
+        # s_memrealtime runs at 100 MHz
+        return {"wait_us": w[0] / 100.0, "exchanges": int(w[1]), "publish_us": w[3] / 100.0}
 
     def check_comm(self):
         """Raise if the in-kernel exchange (xGMI, or the split-batch step's on-chip one)

@@ -98,6 +98,10 @@ def test_bench_strong_scaling_share_gpu(world):
     assert len(rec["exchange_wait_us_per_step_by_rank"]) == world
     assert 0 <= rec["exchange_wait_us_per_step"] <= 1e3 * rec["ms_per_step"]
     assert rec["compute_us_per_step"] > 0
+    # the step three ways: publish, wait, rest
+    assert 0 <= rec["publish_us_per_step"] <= 1e3 * rec["ms_per_step"]
+    assert abs(rec["publish_us_per_step"] + rec["exchange_wait_us_per_step"] + rec["step_rest_us_per_step"]
+               - 1e3 * rec["ms_per_step"]) < 1e-6
     ref = _single_process_full_batch_losses(steps + warmup)
     for got, want in zip(rec["final_loss"], ref):
         assert abs(got - want) <= 1e-3 * abs(want) + 1e-5, (rec["final_loss"], ref)
