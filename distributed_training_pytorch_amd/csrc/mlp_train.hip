@@ -40,6 +40,12 @@ constexpr int kWaves = kBlock / kWave;
 #ifndef DTP_GRP_SPLIT
 #define DTP_GRP_SPLIT 1  // split-batch exchange: publisher / poller waves (grp_allreduce_split); 0: every thread both
 #endif
+#ifndef DTP_GRP_DIRECT
+// 1: the publisher wave sums its granules from the dW tiles itself (no staging, no barrier):
+// measured slower (3.70 vs 3.61 us/step: 24 scattered tile reads on the publisher's path
+// against one LDS round and a barrier, profiles/r5_exchange/direct_ab/)
+#define DTP_GRP_DIRECT 0
+#endif
 
 #ifndef DTP_XWAIT
 #define DTP_XWAIT 1  // 0 (A/B builds only): no exchange-wait diagnostic (bench exchange_wait_us_per_step)
@@ -643,6 +649,22 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     mr[k] = own ? a.opt_m[(size_t)model * P + p] : 0.f;
     vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
   }
+  // split-batch publisher (wave 0, DTP_GRP_DIRECT): the dW-tile positions of the parameters of
+  // its granules q = tid + 64 j (granule q holds parameters NPT (q / GPT) + 2 (q % GPT), + 1;
+  // the last granule is the loss), so it sums them straight from the tiles
+  constexpr int kGpt = xgmi_gpt<NPT>(), kNg = xgmi_nthr(P, NPT) * kGpt + 1, kPubJ = (kNg + kWave - 1) / kWave;
+  int gtp[GRP && DTP_GRP_DIRECT ? kPubJ : 1][2];
+  if constexpr (GRP && DTP_GRP_DIRECT) {
+#pragma unroll
+    for (int j = 0; j < kPubJ; ++j) {
+      const int q = tid + j * kWave;
+      const int p0 = (q / kGpt) * NPT + 2 * (q % kGpt);
+      const bool two = 2 * (q % kGpt) + 1 < NPT;
+      int pf_, pb_;
+      lane_pos<C, S>(p0 < P ? p0 : 0, pf_, pb_, gtp[j][0]);
+      lane_pos<C, S>((two && p0 + 1 < P) ? p0 + 1 : 0, pf_, pb_, gtp[j][1]);
+    }
+  }
   const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
   const bool htab = kAdam && a.adam_tab && a.host_t0 >= 0;
   float2 tabv[kAdamTab / NTH];
@@ -944,7 +966,25 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     if constexpr (GRP && !kXgmi) {  // the members' partial sums, on chip (grp_core.h)
       xepoch += 1u;
       GrpProf gp_;
-#if DTP_GRP_SPLIT
+#if DTP_GRP_SPLIT && DTP_GRP_DIRECT
+      auto pubval = [&](int j) -> float2 {  // granule tid + 64 j of this member, from the tiles
+        float x = 0.f, y = 0.f;
+        if (tid + j * kWave == kNg - 1) {
+#pragma unroll
+          for (int ww = 0; ww < NW; ++ww) x += sm.red[ww][SC::losspos()];
+        } else {
+#pragma unroll
+          for (int ww = 0; ww < NW; ++ww) {
+            x += sm.red[ww][gtp[j][0]];
+            y += sm.red[ww][gtp[j][1]];
+          }
+        }
+        return make_float2(x, y);
+      };
+      lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
+                                              sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr,
+                                              pubval);
+#elif DTP_GRP_SPLIT
       lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
                                               sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr);
 #else
@@ -958,7 +998,10 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
           pr[17] = gp_.t_first;
           pr[31] = gp_.t_end;
           pr[30] = gp_.polls;
+          pr[15] = gp_.rt_end;  // chip-wide clock: this member's last granule
         }
+        if (DTP_GRP_SPLIT && tid == 0 && it < 8)  // the publisher: chip-wide clock when its stores were issued
+          prof[((size_t)blockIdx.x * 8 + it) * 32 + 14] = gp_.rt_pub;
       }
     }
     const float mean_loss = lsum * inv;  // GRP + xGMI: this member's share of the rank's mean
@@ -1247,12 +1290,11 @@ int pick_groups(const DtpTrainArgs& a, int in, int out, bool allow, bool fast1) 
   const int cap = a.smp.world == 1 ? dtp::kGrpMax : dtp::kXgmiMaxWorld / a.smp.world;
   if (gr > cap) return 1;
   if (want == 1) return gr;
-  // the policy (docs/perf_notes.md "Round 5: the split-batch step"): one rank keeps the
-  // one-lane FAST step -- an on-chip hand-off costs ~1 k cycles per memory round trip, 2-3 k
-  // per exchange, about what the split saves; with several ranks the exchange is paid
-  // anyway, so the split's shorter compute shows; and where there is no FAST one-lane
-  // instance (SGD, cross-entropy) the split beats the generic one: on for 4 members per model
-  return ((a.smp.world > 1 || !fast1) && gr >= 4) ? gr : 1;
+  // the policy (docs/perf_notes.md "Round 5: the split-batch step"): on for 4 members per
+  // model (per-rank batch 256 -- one rank: 3.61 vs 4.11 us/step, two ranks: 5.6 vs 6.2-6.6 in
+  // the rehearsal); 2 members (batch 128) measured no better than the 2-lanes step
+  (void)fast1;
+  return gr >= 4 ? gr : 1;
 }
 
 LanePick pick_lanes(const DtpTrainArgs& a, int in, int out, bool fast) {

@@ -30,7 +30,8 @@ def main():
     grouped = "--groups" in sys.argv
     dev = torch.device("cuda", 0)
     X, Y = ToyData(seed=0).device_tensors(dev)
-    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=batch), cfg=EngineConfig())
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=batch),
+                      cfg=EngineConfig(groups="on" if grouped else "auto"))
     tr.train(50)  # warm
     tr.synchronize()
     lib = nat.load()
@@ -57,6 +58,14 @@ def main():
             # XCC id and HW_ID (CU / SIMD / SE bits) of each member of model 0
             res.setdefault("placement", []).append([(int(st[8 * k, 0, 12]), hex(int(st[8 * k, 0, 13])))
                                                     for k in range(tr.groups)])
+            # chip-wide s_memrealtime (10 ns ticks): each member's publish-issued and last-granule
+            # times relative to the first member to publish (skew: the exchange waits for the last)
+            for it in (3, 5):
+                pubs = [int(st[8 * k, it, 14]) for k in range(tr.groups)]
+                ends = [int(st[8 * k, it, 15]) for k in range(tr.groups)]
+                p0 = min(pubs)
+                res.setdefault("realtime_10ns", []).append({"publish": [p - p0 for p in pubs],
+                                                             "last_granule": [e - p0 for e in ends]})
             res.setdefault("exchange_detail", []).append(
                 [{"to_pub": int(st[8 * k, it, 16] - st[8 * k, it, 4]),
                   "pub_to_first_poll": int(st[8 * k, it, 17] - st[8 * k, it, 16]),

@@ -23,6 +23,7 @@ for fn in ("stamps_grp.log", "stamps_grp128.log"):
     print(fn, {k: o[k] for k in ("x_loaded", "fwd+loss", "bwd_done(w0)", "tiles_reduced", "grads_summed", "adam_done",
                                  "step_end", "total_step")})
     print("   placement", obj.get("placement", [None])[-1])
+    print("   realtime", obj.get("realtime_10ns", [None])[-2:])
     for x in obj["exchange_detail"][-1]:
         print("  ", x)
     print("  ", t[i + end:].strip()[:200])
