@@ -84,6 +84,22 @@ DTP_DEV uint32_t grp_check(uint32_t e, uint32_t a, uint32_t b) {
 // granules per (parity, model, member) slot -- the xGMI slot size (xgmi_core.h)
 DTP_HD constexpr int grp_slot16(int P, int npt) { return xgmi_slot16(P, npt); }
 
+#ifndef DTP_GRP_G3
+// 1: the split exchange packs THREE payload floats per 16-byte granule, {epoch ^ h, v0, v1,
+// v2} (the tag word carries the check: a granule passes only as (epoch ^ h) ^ h(v) == epoch,
+// so a stale slot of an earlier epoch never passes and a torn one only on a hash collision):
+// 125 granules per member instead of 187 (toy shape), a third fewer publish stores, and the
+// pollers request exactly their items (2 per lane at 4 members instead of 4)
+#define DTP_GRP_G3 1
+#endif
+// 3-float granules of a member: the P gradients, the loss and the member's XCC id
+DTP_HD constexpr int grp_ng3(int P) { return (P + 2 + 2) / 3; }
+// LDS floats per member of the 3-float form (pub, then one row per member)
+DTP_HD constexpr int grp_ps3(int P) { return (3 * grp_ng3(P) + 3) & ~3; }
+DTP_DEV uint32_t grp_hash3(uint32_t a, uint32_t b, uint32_t c) {
+  return a ^ ((b << 11) | (b >> 21)) ^ ((c << 22) | (c >> 10)) ^ 0x9E3779B9u;
+}
+
 struct GrpCtx {
   void* buf;    // [2][n_models][GR][slot16] granules
   int* status;  // sticky timeout word pair (nullable)
@@ -450,6 +466,185 @@ DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], f
 #pragma unroll
   for (int k = 0; k < NPT; ++k) g[k] = acc[k / 2][k & 1];
   return acc[GPT][0];
+}
+
+// The split exchange with 3-float granules (DTP_GRP_G3, the default).  Same roles and
+// barriers as grp_allreduce_split: the owners stage the member's payload in LDS
+// (lds[0 .. PS): gradients p = 0..P-1, the loss at P, the XCC id at P + 1), wave 0 publishes
+// granule q = floats [3q, 3q + 3) as {epoch ^ h(v), v}, waves 1.. poll the peers' granules
+// into lds[PS (1 + r) ..] with PI items per lane (PI = the lane's share at this member count,
+// two polls in flight), then every thread sums its parameters over the members in order
+// 0..GR-1 (its own value from registers): every member computes the same bits.
+template <int P, int NPT, int NTHREADS>
+DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                                   bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain,
+                                   GrpProf* prof = nullptr) {
+  constexpr int NG = grp_ng3(P), PS = grp_ps3(P);
+  constexpr int NPOLL = NTHREADS - kWave;  // poller lanes (waves 1..)
+  constexpr int slot = grp_slot16(P, NPT);
+  static_assert(NG <= slot, "a member's 3-float granules fit its slot of the exchange buffer");
+  static_assert(NTHREADS > kWave, "one publisher wave and at least one poller wave");
+  float* const pub = lds;
+  float* const peer = lds + PS;  // peer[r * PS + i]: member r's float i
+  const size_t base = (size_t)((int)(epoch & 1u) * c.n_models + model) * c.GR;
+  // 1. the payload into LDS
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (NPT * tid + k < P) pub[NPT * tid + k] = g[k];
+  if (tid == 0) {
+    pub[P] = loss;
+    pub[P + 1] = __uint_as_float(xcc);
+#pragma unroll
+    for (int i = P + 2; i < 3 * NG; ++i) pub[i] = 0.f;
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(c.buf);
+  if (tid < kWave) {
+    // 2a. wave 0 publishes every granule of this member (all its LDS reads first, then the
+    // stores back to back)
+    constexpr int MAXJ = (NG + kWave - 1) / kWave;
+    float v[MAXJ][3];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int q = tid + j * kWave < NG ? tid + j * kWave : NG - 1;
+      v[j][0] = pub[3 * q];
+      v[j][1] = pub[3 * q + 1];
+      v[j][2] = pub[3 * q + 2];
+    }
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int q = tid + j * kWave;
+      if (q < NG) {
+        const uint32_t x0 = __float_as_uint(v[j][0]), x1 = __float_as_uint(v[j][1]), x2 = __float_as_uint(v[j][2]);
+        const u32x4 qq = {epoch ^ grp_hash3(x0, x1, x2), x0, x1, x2};
+        const int off = (int)(((base + c.k) * slot + q) * 16);
+        if (DTP_GRP_SAME_XCD && plain) __builtin_amdgcn_raw_buffer_store_b128(qq, rs, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(qq, rs, off, 0, DTP_GRP_ST_AUX);
+      }
+    }
+    if (prof) {
+      prof->t_pub = grp_clock();
+      prof->rt_pub = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  if (DTP_GRP_PUB_FIRST) __syncthreads();
+  if (tid >= kWave) {
+    // 2b. item i = (peer index i / NG, granule i % NG), lane pl holds items pl + j NPOLL
+    const int pl = tid - kWave;
+    const int total = (c.GR - 1) * NG;
+    unsigned long long deadline = 0;
+    unsigned spins = 0;
+    if (prof) prof->t_pub = grp_clock();
+    auto expired = [&]() {
+      if ((++spins & 63u) != 0u) return false;
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (!deadline) {
+        deadline = now + (unsigned long long)(c.timeout_us > 0 ? c.timeout_us : 2000000) * 100ull;
+      } else if (now > deadline) {
+        if (c.status) {
+          atomicExch(&c.status[0], 1);
+          atomicExch(&c.status[1], (int)epoch);
+        }
+        return true;
+      }
+      return false;
+    };
+    // PI items per lane, two polls in flight; every poll requests all PI items (a fixed load
+    // count keeps the waits counted), absent items read offset 0
+    auto run = [&](auto PIC) {
+      constexpr int PI = decltype(PIC)::value;
+      int off[PI], dst[PI];
+      uint32_t pending = 0u;
+#pragma unroll
+      for (int j = 0; j < PI; ++j) {
+        const int i = pl + j * NPOLL;
+        const int ri = i / NG, q = i - ri * NG;
+        const int r = ri < c.k ? ri : ri + 1;
+        const bool in = i < total;
+        off[j] = in ? (int)(((base + r) * slot + q) * 16) : 0;
+        dst[j] = r * PS + 3 * q;
+        if (in) pending |= 1u << j;
+      }
+      auto issue = [&](u32x4 (&x)[PI]) {
+        asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
+#pragma unroll
+        for (int j = 0; j < PI; ++j) x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, DTP_GRP_LD_AUX);
+      };
+      auto consume = [&](const u32x4 (&x)[PI]) {
+#pragma unroll
+        for (int j = 0; j < PI; ++j) {
+          if (((pending >> j) & 1u) && (x[j].x ^ grp_hash3(x[j].y, x[j].z, x[j].w)) == epoch) {
+            float* d = peer + dst[j];
+            d[0] = __uint_as_float(x[j].y);
+            d[1] = __uint_as_float(x[j].z);
+            d[2] = __uint_as_float(x[j].w);
+            pending &= ~(1u << j);
+          }
+        }
+      };
+      u32x4 xa[PI], xb[PI];
+      if (!DTP_GRP_PIPE) {  // one poll in flight (A/B)
+        while (pending && !dead) {
+          issue(xa);
+          consume(xa);
+          if (prof && spins == 0) prof->t_first = grp_clock();
+          if (pending && expired()) dead = true;
+        }
+        return;
+      }
+      if (pending && !dead) issue(xa);
+      while (pending && !dead) {
+        issue(xb);
+        consume(xa);
+        if (prof && spins == 0) prof->t_first = grp_clock();
+        if (!pending) break;
+        if (expired()) {
+          dead = true;
+          break;
+        }
+        issue(xa);
+        consume(xb);
+        if (!pending) break;
+        if (expired()) {
+          dead = true;
+          break;
+        }
+      }
+    };
+    constexpr int MAXI = ((kGrpMax - 1) * NG + NPOLL - 1) / NPOLL;
+    const int pi = (total + NPOLL - 1) / NPOLL;
+    if (pi <= 1) run(std::integral_constant<int, 1>{});
+    else if (pi <= 2) run(std::integral_constant<int, 2>{});
+    else if (pi <= 3) run(std::integral_constant<int, 3>{});
+    else run(std::integral_constant<int, MAXI>{});
+    if (prof) {
+      prof->t_end = grp_clock();
+      prof->polls = spins + 1;
+      prof->rt_end = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __syncthreads();
+  // 3. member-order sums
+  if (DTP_GRP_SAME_XCD && !plain && !dead) {  // every member on this XCD: plain stores from the next exchange on
+    bool same = true;
+    for (int r = 0; r < c.GR; ++r)
+      if (r != c.k) same = same && __float_as_uint(peer[r * PS + P + 1]) == xcc;
+    plain = same;
+  }
+  float acc[NPT], lacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) acc[k] = 0.f;
+  const int p0 = NPT * tid < P ? NPT * tid : 0;
+  for (int r = 0; r < c.GR; ++r) {
+    const float* row = peer + r * PS;
+    const bool me = r == c.k;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) acc[k] += me ? g[k] : row[p0 + k];
+    lacc += me ? loss : row[P];
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) g[k] = acc[k];
+  return lacc;
 }
 
 }  // namespace dtp

@@ -584,7 +584,10 @@ struct LaneSmem {
   float sink[4];
   // split-batch exchange (grp_allreduce_split): this member's payloads, then every member's
   static constexpr int GSLOT = xgmi_slot16(S::P, (S::P + 64 * NW - 1) / (64 * NW));
-  alignas(16) float2 gx[GRP ? (kGrpMax + 1) * GSLOT : 2];
+  // (the 3-float form, DTP_GRP_G3: (kGrpMax + 1) rows of grp_ps3(P) floats)
+  static constexpr int GX2 = (kGrpMax + 1) * GSLOT > (kGrpMax + 1) * grp_ps3(S::P) / 2
+                                 ? (kGrpMax + 1) * GSLOT : (kGrpMax + 1) * grp_ps3(S::P) / 2;
+  alignas(16) float2 gx[GRP ? GX2 : 2];
 };
 
 // NW waves per workgroup (4: one per SIMD; 8: two per SIMD, for batches of 256 / L < B <= 512 / L)
@@ -984,6 +987,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
                                               sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr,
                                               pubval);
+#elif DTP_GRP_SPLIT && DTP_GRP_G3
+      lsum = grp_allreduce_split3<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, reinterpret_cast<float*>(sm.gx),
+                                               xcc, gplain, PROF ? &gp_ : nullptr);
 #elif DTP_GRP_SPLIT
       lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
                                               sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr);

@@ -3,8 +3,12 @@
 // primitive under the split-batch step's exchange (csrc/grp_core.h).
 // Ping-pong: A stores epoch e into granule 0 (16 B), B polls until it sees e, stores e
 // into granule 1, A polls for it; N round trips, timed with s_memtime on A.
-// Variants: store cache bits (0 = plain, 16 = sc1) x lanes per poll (1 lane, or a whole
-// wave polling 64 contiguous granules, as the exchange's poller waves do).
+// Variants: store cache bits (0 = plain, 16 = sc1) x poll-load cache bits (16 = sc1, 1 = sc0,
+// 17 = sc0 sc1) x lanes per poll (1 lane, or a whole wave polling 64 contiguous granules, as
+// the exchange's poller waves do).  A load form that can hit a stale line in the CU's L1
+// never sees the peer's epoch: its run ends at the spin bound and prints "stale".
+// Second part: dependent-load latency (one lane, a pointer chase over 64 lines that stay in
+// L2) per load cache-bit form.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -15,7 +19,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7fffffff, 0x00020000);
 }
 
-template <int ST, bool WAVE>
+template <int ST, bool WAVE, int LD = 16>
 __global__ void pingpong(void* buf, int peer_block, int n, unsigned long long* out) {
   const int b = blockIdx.x;
   if (b != 0 && b != peer_block) return;
@@ -33,7 +37,7 @@ __global__ void pingpong(void* buf, int peer_block, int n, unsigned long long* o
       unsigned long long spins = 0;
       while (true) {
         asm volatile("" ::: "memory");
-        u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, peer_off, 0, 16);
+        u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, peer_off, 0, LD);
         if (__all((int)(x.x == (unsigned)e))) break;
         if (++spins > 2000000ull) return;  // bounded: a lost hand-off ends the kernel
       }
@@ -41,7 +45,7 @@ __global__ void pingpong(void* buf, int peer_block, int n, unsigned long long* o
       unsigned long long spins = 0;
       while (true) {
         asm volatile("" ::: "memory");
-        u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, peer_off, 0, 16);
+        u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, peer_off, 0, LD);
         if (__all((int)(x.x == (unsigned)e))) break;
         if (++spins > 2000000ull) return;  // bounded: a lost hand-off ends the kernel
       }
@@ -61,22 +65,49 @@ __global__ void pingpong(void* buf, int peer_block, int n, unsigned long long* o
   }
 }
 
-template <int ST, bool WAVE>
+template <int ST, bool WAVE, int LD = 16>
 void run(const char* name, void* buf, unsigned long long* d_out, int peer) {
   const int n = 2000;
   (void)hipMemset(buf, 0, 8192);
   (void)hipMemset(d_out, 0, 64);
-  hipLaunchKernelGGL((pingpong<ST, WAVE>), dim3(16), dim3(64), 0, 0, buf, peer, n, d_out);
+  hipLaunchKernelGGL((pingpong<ST, WAVE, LD>), dim3(16), dim3(64), 0, 0, buf, peer, n, d_out);
   unsigned long long h[3];
   (void)hipMemcpy(h, d_out, sizeof h, hipMemcpyDeviceToHost);
-  printf("{\"variant\": \"%s\", \"peer_block\": %d, \"xcc\": [%llu, %llu], \"cycles_per_round_trip\": %.1f}\n", name, peer,
-         h[1], h[2], (double)h[0] / n);
+  if (!h[0]) printf("{\"variant\": \"%s\", \"peer_block\": %d, \"stale\": true}\n", name, peer);
+  else
+    printf("{\"variant\": \"%s\", \"peer_block\": %d, \"xcc\": [%llu, %llu], \"cycles_per_round_trip\": %.1f}\n", name,
+           peer, h[1], h[2], (double)h[0] / n);
+}
+
+// one lane chases next = buf[cur].x over 64 lines (16 KB, L2-resident after the first lap)
+template <int LD>
+__global__ void chase(void* buf, int n, unsigned long long* out) {
+  if (threadIdx.x != 0) return;
+  __amdgpu_buffer_rsrc_t rs = rsrc(buf);
+  unsigned off = 0;
+  for (int i = 0; i < 64; ++i) { const u32x4 v_ = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, LD); off = v_.x; }  // warm lap
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < n; ++i) { const u32x4 v_ = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, LD); off = v_.x; }
+  out[0] = __builtin_amdgcn_s_memtime() - t0;
+  out[1] = off;
+}
+
+template <int LD>
+void run_chase(const char* name, void* buf, unsigned long long* d_out) {
+  const int n = 4096;
+  unsigned h_init[64 * 64] = {};
+  for (int i = 0; i < 64; ++i) h_init[i * 64] = ((i * 37 + 1) % 64) * 256;  // line i -> line (37 i + 1) mod 64
+  (void)hipMemcpy(buf, h_init, sizeof h_init, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL((chase<LD>), dim3(1), dim3(64), 0, 0, buf, n, d_out);
+  unsigned long long h[2];
+  (void)hipMemcpy(h, d_out, sizeof h, hipMemcpyDeviceToHost);
+  printf("{\"chase\": \"%s\", \"cycles_per_load\": %.1f}\n", name, (double)h[0] / n);
 }
 
 int main() {
   void* buf;
   unsigned long long* d_out;
-  (void)hipMalloc(&buf, 8192);
+  (void)hipMalloc(&buf, 65536);
   (void)hipMalloc(&d_out, 64);
   for (int peer : {8, 1}) {
     run<16, false>("sc1 store, 1 lane", buf, d_out, peer);
@@ -84,5 +115,13 @@ int main() {
     run<16, true>("sc1 store, 64 lanes x 16 B", buf, d_out, peer);
     if (peer == 8) run<0, true>("plain store, 64 lanes x 16 B", buf, d_out, peer);
   }
+  run<0, false, 1>("plain store, sc0 poll, 1 lane", buf, d_out, 8);
+  run<0, false, 17>("plain store, sc0 sc1 poll, 1 lane", buf, d_out, 8);
+  run<0, true, 1>("plain store, sc0 poll, 64 lanes x 16 B", buf, d_out, 8);
+  run<0, true, 17>("plain store, sc0 sc1 poll, 64 lanes x 16 B", buf, d_out, 8);
+  run_chase<0>("plain", buf, d_out);
+  run_chase<1>("sc0", buf, d_out);
+  run_chase<16>("sc1", buf, d_out);
+  run_chase<17>("sc0 sc1", buf, d_out);
   return 0;
 }
