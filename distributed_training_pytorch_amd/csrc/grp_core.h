@@ -92,6 +92,18 @@ DTP_HD constexpr int grp_slot16(int P, int npt) { return xgmi_slot16(P, npt); }
 // pollers request exactly their items (2 per lane at 4 members instead of 4)
 #define DTP_GRP_G3 1
 #endif
+#ifndef DTP_GRP_OVERLAP
+// 1: the caller's exchange-independent work (next sample gather, index request) runs inside
+// the exchange's waits (grp_allreduce_split3's ov).  Measured slower: 3.90-3.92 vs 3.40 us/step
+// (profiles/r5_exchange/overlap/) -- the wait counts around the polls lose their slack
+#define DTP_GRP_OVERLAP 0
+#endif
+#ifndef DTP_GRP_PIPE3
+// the 3-float form's pollers: 0 = one poll in flight, 1 = two.  With 2 items per lane one poll
+// measured faster (3.40 vs 3.44-3.46 us/step, profiles/r5_exchange/g3/); the 2-float form
+// (4 items per lane) gained from two
+#define DTP_GRP_PIPE3 0
+#endif
 // 3-float granules of a member: the P gradients, the loss and the member's XCC id
 DTP_HD constexpr int grp_ng3(int P) { return (P + 2 + 2) / 3; }
 // LDS floats per member of the 3-float form (pub, then one row per member)
@@ -475,10 +487,14 @@ DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], f
 // into lds[PS (1 + r) ..] with PI items per lane (PI = the lane's share at this member count,
 // two polls in flight), then every thread sums its parameters over the members in order
 // 0..GR-1 (its own value from registers): every member computes the same bits.
-template <int P, int NPT, int NTHREADS>
+// ov(): the caller's work that does not depend on the exchange (the next step's sample
+// gather and index request), run exactly once by every thread while its memory requests are
+// in flight: the publisher after its stores, a poller between its first poll's issue and
+// its consumption.
+template <int P, int NPT, int NTHREADS, class OverlapFn>
 DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
-                                   bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain,
-                                   GrpProf* prof = nullptr) {
+                                   bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain, GrpProf* prof,
+                                   OverlapFn ov) {
   constexpr int NG = grp_ng3(P), PS = grp_ps3(P);
   constexpr int NPOLL = NTHREADS - kWave;  // poller lanes (waves 1..)
   constexpr int slot = grp_slot16(P, NPT);
@@ -526,6 +542,7 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
       prof->t_pub = grp_clock();
       prof->rt_pub = __builtin_amdgcn_s_memrealtime();
     }
+    if (DTP_GRP_OVERLAP) ov();
   }
   if (DTP_GRP_PUB_FIRST) __syncthreads();
   if (tid >= kWave) {
@@ -549,8 +566,8 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
       }
       return false;
     };
-    // PI items per lane, two polls in flight; every poll requests all PI items (a fixed load
-    // count keeps the waits counted), absent items read offset 0
+    // PI items per lane (one or two polls in flight, DTP_GRP_PIPE3); every poll requests all PI
+    // items (a fixed load count keeps the waits counted), absent items read offset 0
     auto run = [&](auto PIC) {
       constexpr int PI = decltype(PIC)::value;
       int off[PI], dst[PI];
@@ -583,16 +600,26 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
         }
       };
       u32x4 xa[PI], xb[PI];
-      if (!DTP_GRP_PIPE) {  // one poll in flight (A/B)
+      bool ovd = !DTP_GRP_OVERLAP;
+      if (!DTP_GRP_PIPE3) {  // one poll in flight (the default with 3-float granules)
         while (pending && !dead) {
           issue(xa);
+          if (!ovd) {
+            ov();
+            ovd = true;
+          }
           consume(xa);
           if (prof && spins == 0) prof->t_first = grp_clock();
           if (pending && expired()) dead = true;
         }
+        if (!ovd) ov();
         return;
       }
       if (pending && !dead) issue(xa);
+      if (!ovd) {
+        ov();
+        ovd = true;
+      }
       while (pending && !dead) {
         issue(xb);
         consume(xa);

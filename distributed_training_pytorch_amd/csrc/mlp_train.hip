@@ -966,6 +966,17 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     float lsum = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::losspos()];
+    // the next step's sample and the index of the one after it (independent of this step's
+    // exchange: the split-batch step runs it inside the exchange's waits)
+    const int lslot_now = lslot;
+    auto next_sample = [&]() {
+      roll(epoch, bi);
+      if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
+      nvalid = fast_gather(fidx, nx, ny);
+      roll(e2, b2);
+      fidx = fast_index(e2, b2);
+    };
+    bool sampled = false;
     if constexpr (GRP && !kXgmi) {  // the members' partial sums, on chip (grp_core.h)
       xepoch += 1u;
       GrpProf gp_;
@@ -989,7 +1000,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
                                               pubval);
 #elif DTP_GRP_SPLIT && DTP_GRP_G3
       lsum = grp_allreduce_split3<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, reinterpret_cast<float*>(sm.gx),
-                                               xcc, gplain, PROF ? &gp_ : nullptr);
+                                               xcc, gplain, PROF ? &gp_ : nullptr, next_sample);
+      sampled = DTP_GRP_OVERLAP;
 #elif DTP_GRP_SPLIT
       lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
                                               sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr);
@@ -1025,12 +1037,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
                                                GRP ? a.groups : 1, gk, &xdead);
       }
     }
-    const int lslot_now = lslot;
-    roll(epoch, bi);
-    if (a.loss_log && ++lslot == a.loss_log_cap) lslot = 0;
-    nvalid = fast_gather(fidx, nx, ny);
-    roll(e2, b2);
-    fidx = fast_index(e2, b2);
+    if (!sampled) next_sample();
     {
       AdamScalars as = adam_consts(a.hp);
       as.step_size = adam_sc.x;
