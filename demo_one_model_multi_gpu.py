@@ -15,10 +15,14 @@ TASKS_PER_NODE=1).  Two engines:
   its GPU's receive buffer over xGMI; each stage's gradient is all-reduced over
   the DP ranks inside its kernel (per-device buckets); Adam / SGD fused.
 * ``--engine module``: the autograd path -- stage kernels whose epilogue stores the
-  activation into the next GPU, optional GPipe micro-batches (``--microbatches``),
-  per-device DDP buckets reduced from grad-ready hooks (``LayerSplitDDP``).
-Configurations the persistent kernels do not cover (micro-batches, batch > 256,
-other losses) fall back to ``module`` with a printed reason.  Both engines draw the
+  activation into the next GPU, GPipe micro-batches in wavefront issue order
+  (``--microbatches``), per-device DDP buckets reduced from grad-ready hooks
+  (``LayerSplitDDP``).
+``--microbatches M`` on the fused engine: the stage kernels hand every sample over its
+own link granules, so each wave's 64 samples cross the stages as an independent
+micro-batch; the math is GPipe's (full-batch gradient, one optimizer step per
+iteration), M only regroups the samples.  Configurations the persistent kernels do not
+cover (batch > 256, other losses) fall back to ``module`` with a printed reason.  Both engines draw the
 reference's exact DistributedSampler order by default (``--sampler torch``).
 Checkpoint / resume (``--checkpoint_dir --checkpoint_every --resume``) works for
 both.  Launch with torchrun (``--torchrun``) or plain srun exactly like demo.py.
@@ -76,8 +80,6 @@ def _fused_reason(config, devs) -> str | None:
         return f"--engine {config.engine}"
     if devs[0].type != "cuda" or not nat.native_enabled():
         return "CPU run"
-    if config.microbatches > 1:
-        return "GPipe micro-batches run on the autograd path"
     if config.batch_size > 256:
         return "per-rank batch > 256 (one lane per sample)"
     if config.loss != "mse":
@@ -122,6 +124,14 @@ def main(argv=None):
             why, eng = str(e), None
     if why is None:
         rank_print(rank, f"engine: fused layer split ({len(devs)} persistent stage kernels)")
+        if config.microbatches > 1:
+            # GPipe semantics are the full-batch gradient and one optimizer step per iteration
+            # (LayerSplitMLP concatenates the micro-batch outputs before the loss); the stage
+            # kernels hand every sample over its own link granules, so each wave's 64 samples
+            # already cross the stages as an independent micro-batch -- M only regroups them
+            rank_print(rank, f"micro-batches: {config.microbatches} requested; the stage kernels stream "
+                             "every wave's 64 samples through the links independently (same gradient, "
+                             "one optimizer step per iteration)")
         summary = _run_fused(config, eng, geom, world, rank, logger, faults, pbar)
     else:
         if config.engine == "fused":

@@ -674,4 +674,140 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
   return lacc;
 }
 
+#ifndef DTP_GRP_DIRECT3
+// 1: the 3-float exchange publishes straight from the per-wave dW tiles (grp_allreduce_split3d):
+// no staging pass, no staging barrier.  Measured slower: 3.50 vs 3.35-3.36 us/step
+// (profiles/r5_exchange/direct3/): the publish leaves ~300 cycles earlier, but two poller
+// waves with 3 items per lane end later than three with 2
+#define DTP_GRP_DIRECT3 0
+#endif
+
+// The 3-float exchange without the staging pass.  Right after the tile-park barrier, lane q
+// of the first ceil(NG / 64) waves forms granule q itself (pub3(q): the wave-order sums of
+// its three payload floats, straight from the parked tiles) and stores it; the other waves
+// form their own parameters' sums meanwhile (own()), then poll after the publisher-first
+// barrier while the publishers form theirs.  Same member-order sums as grp_allreduce_split3,
+// so the same bits on every member -- as long as pub3 and own sum the waves in the same order.
+template <int P, int NPT, int NTHREADS, class Pub3Fn, class OwnFn>
+DTP_DEV float grp_allreduce_split3d(const GrpCtx& c, int model, float (&g)[NPT], const float& loss, unsigned epoch,
+                                    int tid, bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain,
+                                    GrpProf* prof, Pub3Fn pub3, OwnFn own) {
+  constexpr int NG = grp_ng3(P), PS = grp_ps3(P);
+  constexpr int NPUB = ((NG + kWave - 1) / kWave) * kWave;  // publisher lanes (whole waves)
+  constexpr int NPOLL = NTHREADS - NPUB;                    // poller lanes
+  constexpr int slot = grp_slot16(P, NPT);
+  static_assert(NG <= slot, "a member's 3-float granules fit its slot of the exchange buffer");
+  static_assert(NPOLL >= kWave, "at least one poller wave");
+  float* const peer = lds;  // peer[r * PS + i]: member r's float i (this member's row unused)
+  const size_t base = (size_t)((int)(epoch & 1u) * c.n_models + model) * c.GR;
+  const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(c.buf);
+  if (tid < NPUB) {
+    if (tid < NG) {
+      float v[3];
+      pub3(tid, v);
+      const uint32_t x0 = __float_as_uint(v[0]), x1 = __float_as_uint(v[1]), x2 = __float_as_uint(v[2]);
+      const u32x4 qq = {epoch ^ grp_hash3(x0, x1, x2), x0, x1, x2};
+      const int off = (int)(((base + c.k) * slot + tid) * 16);
+      if (DTP_GRP_SAME_XCD && plain) __builtin_amdgcn_raw_buffer_store_b128(qq, rs, off, 0, 0);
+      else __builtin_amdgcn_raw_buffer_store_b128(qq, rs, off, 0, DTP_GRP_ST_AUX);
+    }
+    if (prof) {
+      prof->t_pub = grp_clock();
+      prof->rt_pub = __builtin_amdgcn_s_memrealtime();
+    }
+  } else {
+    own();
+  }
+  if (DTP_GRP_PUB_FIRST) __syncthreads();
+  if (tid >= NPUB) {
+    const int pl = tid - NPUB;
+    const int total = (c.GR - 1) * NG;
+    unsigned long long deadline = 0;
+    unsigned spins = 0;
+    if (prof) prof->t_pub = grp_clock();
+    auto expired = [&]() {
+      if ((++spins & 63u) != 0u) return false;
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (!deadline) {
+        deadline = now + (unsigned long long)(c.timeout_us > 0 ? c.timeout_us : 2000000) * 100ull;
+      } else if (now > deadline) {
+        if (c.status) {
+          atomicExch(&c.status[0], 1);
+          atomicExch(&c.status[1], (int)epoch);
+        }
+        return true;
+      }
+      return false;
+    };
+    auto run = [&](auto PIC) {
+      constexpr int PI = decltype(PIC)::value;
+      int off[PI], dst[PI];
+      uint32_t pending = 0u;
+#pragma unroll
+      for (int j = 0; j < PI; ++j) {
+        const int i = pl + j * NPOLL;
+        const int ri = i / NG, q = i - ri * NG;
+        const int r = ri < c.k ? ri : ri + 1;
+        const bool in = i < total;
+        off[j] = in ? (int)(((base + r) * slot + q) * 16) : 0;
+        dst[j] = r * PS + 3 * q;
+        if (in) pending |= 1u << j;
+      }
+      while (pending && !dead) {
+        u32x4 x[PI];
+        asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
+#pragma unroll
+        for (int j = 0; j < PI; ++j) x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, DTP_GRP_LD_AUX);
+#pragma unroll
+        for (int j = 0; j < PI; ++j) {
+          if (((pending >> j) & 1u) && (x[j].x ^ grp_hash3(x[j].y, x[j].z, x[j].w)) == epoch) {
+            float* d = peer + dst[j];
+            d[0] = __uint_as_float(x[j].y);
+            d[1] = __uint_as_float(x[j].z);
+            d[2] = __uint_as_float(x[j].w);
+            pending &= ~(1u << j);
+          }
+        }
+        if (prof && spins == 0) prof->t_first = grp_clock();
+        if (pending && expired()) dead = true;
+      }
+    };
+    constexpr int MAXI = ((kGrpMax - 1) * NG + NPOLL - 1) / NPOLL;
+    const int pi = (total + NPOLL - 1) / NPOLL;
+    if (pi <= 1) run(std::integral_constant<int, 1>{});
+    else if (pi <= 2) run(std::integral_constant<int, 2>{});
+    else if (pi <= 3) run(std::integral_constant<int, 3>{});
+    else if (pi <= 4) run(std::integral_constant<int, 4>{});
+    else run(std::integral_constant<int, MAXI>{});
+    if (prof) {
+      prof->t_end = grp_clock();
+      prof->polls = spins + 1;
+      prof->rt_end = __builtin_amdgcn_s_memrealtime();
+    }
+  } else {
+    own();
+  }
+  __syncthreads();
+  if (DTP_GRP_SAME_XCD && !plain && !dead) {  // every member on this XCD: plain stores from the next exchange on
+    bool same = true;
+    for (int r = 0; r < c.GR; ++r)
+      if (r != c.k) same = same && __float_as_uint(peer[r * PS + P + 1]) == xcc;
+    plain = same;
+  }
+  float acc[NPT], lacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) acc[k] = 0.f;
+  const int p0 = NPT * tid < P ? NPT * tid : 0;
+  for (int r = 0; r < c.GR; ++r) {
+    const float* row = peer + r * PS;
+    const bool me = r == c.k;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) acc[k] += me ? g[k] : row[p0 + k];
+    lacc += me ? loss : row[P];
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) g[k] = acc[k];
+  return lacc;
+}
+
 }  // namespace dtp

@@ -668,6 +668,19 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       lane_pos<C, S>((two && p0 + 1 < P) ? p0 + 1 : 0, pf_, pb_, gtp[j][1]);
     }
   }
+  // split-batch direct publish (DTP_GRP_DIRECT3): the dW-tile positions of the payload floats
+  // 3 tid .. 3 tid + 2 of granule tid (a parameter's tile slot, the loss slot, or -1: the XCC
+  // id / padding)
+  int gt3[GRP && DTP_GRP_DIRECT3 ? 3 : 1];
+  if constexpr (GRP && DTP_GRP_DIRECT3) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int f = 3 * tid + i;
+      int pf_, pb_, t_;
+      lane_pos<C, S>(f < P ? f : 0, pf_, pb_, t_);
+      gt3[i] = f < P ? t_ : (f == P ? SC::losspos() : -1);
+    }
+  }
   const int t0 = a.host_t0 >= 0 ? a.host_t0 : a.step[model];
   const bool htab = kAdam && a.adam_tab && a.host_t0 >= 0;
   float2 tabv[kAdamTab / NTH];
@@ -956,16 +969,24 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     const float2 adam_sc = kAdam ? sm.adam_tab[it % kAdamTab] : make_float2(0.f, 1.f);
     DTP_STAMP(4);
     float g[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) s += sm.red[ww][tp[k]];
-      g[k] = s;
-    }
     float lsum = 0.f;
+    // this thread's parameters summed over the waves (and the loss), in wave order
+    auto own_sums = [&]() {
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) lsum += sm.red[ww][SC::losspos()];
+      for (int k = 0; k < NPT; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) s += sm.red[ww][tp[k]];
+        g[k] = s;
+      }
+      float ls = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) ls += sm.red[ww][SC::losspos()];
+      lsum = ls;
+    };
+    // the split-batch step's direct publish forms these inside the exchange
+    constexpr bool kDefer = GRP && !kXgmi && DTP_GRP_SPLIT && DTP_GRP_G3 && DTP_GRP_DIRECT3;
+    if constexpr (!kDefer) own_sums();
     // the next step's sample and the index of the one after it (independent of this step's
     // exchange: the split-batch step runs it inside the exchange's waits)
     const int lslot_now = lslot;
@@ -998,6 +1019,23 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       lsum = grp_allreduce_split<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, sm.gx,
                                               sm.gx + xgmi_slot16(P, NPT), xcc, gplain, PROF ? &gp_ : nullptr,
                                               pubval);
+#elif DTP_GRP_SPLIT && DTP_GRP_G3 && DTP_GRP_DIRECT3
+      // granule q = tid: payload floats 3q .. 3q + 2 summed over the waves' parked tiles in
+      // wave order (own_sums' order: the published values are the bits this member adds)
+      auto pub3 = [&](int q, float (&v)[3]) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int pos = gt3[i] >= 0 ? gt3[i] : 0;
+          float s_ = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < NW; ++ww) s_ += sm.red[ww][pos];
+          const int f = 3 * q + i;
+          v[i] = f == P + 1 ? __uint_as_float(xcc) : (gt3[i] >= 0 ? s_ : 0.f);
+        }
+      };
+      lsum = grp_allreduce_split3d<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead,
+                                                reinterpret_cast<float*>(sm.gx), xcc, gplain,
+                                                PROF ? &gp_ : nullptr, pub3, own_sums);
 #elif DTP_GRP_SPLIT && DTP_GRP_G3
       lsum = grp_allreduce_split3<P, NPT, NTH>(gctx, model, g, lsum, xepoch, tid, xdead, reinterpret_cast<float*>(sm.gx),
                                                xcc, gplain, PROF ? &gp_ : nullptr, next_sample);

@@ -89,11 +89,27 @@ def test_demo_mpiexec_env_on_gpu(tmp_path):
 
 
 def test_demo_layer_split_pipeline_on_gpu(tmp_path):
+    """GPipe micro-batches on the autograd layer split (wavefront issue order)."""
     out = _run(["demo_one_model_multi_gpu.py", "--gpus_per_proc", "2", "--microbatches", "2", "--allow_shared_gpu",
-                "--iters", "200", "--seed", "0", "--dry_run", "--no_progress", "--log_dir", str(tmp_path)])
+                "--engine", "module", "--iters", "200", "--seed", "0", "--dry_run", "--no_progress",
+                "--log_dir", str(tmp_path)])
     s = _summary(out)
     assert s["stages"] == 2 and s["microbatches"] == 2 and s["iters"] == 200
     assert 0.0 < s["final_loss"] < 4.0, s
+
+
+def test_demo_layer_split_microbatches_on_fused_engine(tmp_path):
+    """--microbatches on the default engine runs the persistent stage kernels (each wave's
+    samples cross the links as their own micro-batch): the same math as M = 1, so the
+    losses are bitwise those of the unmicro-batched run."""
+    base = ["demo_one_model_multi_gpu.py", "--gpus_per_proc", "2", "--allow_shared_gpu", "--iters", "300",
+            "--seed", "0", "--dry_run", "--no_progress"]
+    out2 = _run(base + ["--microbatches", "2", "--log_dir", str(tmp_path / "m2")])
+    out1 = _run(base + ["--log_dir", str(tmp_path / "m1")])
+    assert "engine: fused layer split" in out2 and "micro-batches: 2 requested" in out2, out2[-2000:]
+    s2, s1 = _summary(out2), _summary(out1)
+    assert s2["engine"] == "split-fused" and s2["microbatches"] == 2
+    assert s2["final_loss"] == s1["final_loss"], (s2, s1)
 
 
 def test_demo_lightning_trainer_on_gpu(tmp_path):
