@@ -1342,7 +1342,7 @@ int pick_groups(const DtpTrainArgs& a, int in, int out, bool allow, bool fast1) 
   if (gr > cap) return 1;
   if (want == 1) return gr;
   // the policy (docs/perf_notes.md "Round 5: the split-batch step"): on for 4 members per
-  // model (per-rank batch 256 -- one rank: 3.61 vs 4.11 us/step, two ranks: 5.6 vs 6.2-6.6 in
+  // model (per-rank batch 256 -- one rank: 3.35-3.40 vs 4.11 us/step, two ranks: 5.6 vs 6.2-6.6 in
   // the rehearsal); 2 members (batch 128) measured no better than the 2-lanes step
   (void)fast1;
   return gr >= 4 ? gr : 1;
