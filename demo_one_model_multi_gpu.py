@@ -41,6 +41,7 @@ from distributed_training_pytorch_amd.data.sampler import BatchIndexer, SamplerG
 from distributed_training_pytorch_amd.data.toy_data import ToyData  # noqa: E402
 from distributed_training_pytorch_amd.engine import runner  # noqa: E402
 from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
+from distributed_training_pytorch_amd.ops.loss import MSELoss  # noqa: E402
 from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig  # noqa: E402
 from distributed_training_pytorch_amd.parallel import comm_util  # noqa: E402
 from distributed_training_pytorch_amd.parallel.layer_split import (FusedLayerSplit, LayerSplitDDP,  # noqa: E402
@@ -220,7 +221,7 @@ def _run_module(config, toy, devs, bounds, ds, geom, ocfg, world, rank, logger, 
     X, Y = ds.device_tensors(devs[0])
     Yl = Y.to(devs[-1])
     indexer = BatchIndexer(geom, devs[0], exact_torch=config.sampler == "torch")
-    lossf = torch.nn.MSELoss()
+    lossf = MSELoss()  # nn.MSELoss drop-in, one fused launch each way (ops/loss.py)
     start = 0
     if config.resume and config.checkpoint_dir:
         st = checkpoint.load(config.checkpoint_dir)

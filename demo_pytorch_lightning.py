@@ -18,6 +18,7 @@ import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
 from torch.utils.data import DataLoader  # noqa: E402
 
+from distributed_training_pytorch_amd.ops.loss import MSELoss  # noqa: E402
 from distributed_training_pytorch_amd.runtime.errors import record  # noqa: E402
 from distributed_training_pytorch_amd.trainer import LightningModule, Trainer  # noqa: E402
 from toy_model_and_data import ToyData, ToyModel  # noqa: E402
@@ -28,7 +29,7 @@ class LitToyModel(LightningModule):
         super().__init__()
         self.model_X = ToyModel()
         self.model_Y = ToyModel()
-        self.loss = nn.MSELoss()
+        self.loss = MSELoss()  # nn.MSELoss drop-in: one fused launch each way (ops/loss.py)
         self.lr = lr
 
     def forward(self, x):

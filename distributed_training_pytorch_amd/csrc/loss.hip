@@ -1,0 +1,73 @@
+// Fused MSE loss for the module (autograd) path: what nn.MSELoss(reduction="mean") does
+// in the reference's training step (demo.py:103-104, demo_pytorch_lightning.py:27-33) as
+// ONE launch forward and ONE backward, instead of torch's elementwise square + mean
+// reduction forward (2 launches) and its backward.  The Trainer replays a batch's
+// optimizer steps as a hipGraph, where every launch costs ~4 us whatever it does
+// (profiles/r4_lightning_module/), so the launch count is the cost.
+//
+// forward: one workgroup of 256 threads (the toy batches are <= a few thousand
+// elements); each lane sums (a - b)^2 over a grid stride, then a wave butterfly (DPP row
+// and swizzle-free shuffles) and the 4 wave partials in LDS; out = sum / n.
+// backward: ga = g * 2 (a - b) / n (and gb = -ga when the target needs a gradient); g is
+// read on the device (no host sync in a captured graph).
+#include "dtp_api.h"
+#include "dtp_common.h"
+
+namespace dtp {
+
+__global__ __launch_bounds__(kBlock) void mse_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         long long n, float inv_n, float* __restrict__ out) {
+  __shared__ float part[kBlock / kWave];
+  const int tid = threadIdx.x;
+  float s = 0.f;
+  for (long long i = tid; i < n; i += kBlock) {
+    const float d = a[i] - b[i];
+    s = fmaf(d, d, s);
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+  if ((tid & (kWave - 1)) == 0) part[tid / kWave] = s;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBlock / kWave; ++w) t += part[w];
+    out[0] = t * inv_n;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mse_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         const float* __restrict__ g, long long n, float scale,
+                                                         float* __restrict__ ga, float* __restrict__ gb) {
+  const float gs = g[0] * scale;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+    const float d = gs * (a[i] - b[i]);
+    if (ga) ga[i] = d;
+    if (gb) gb[i] = -d;
+  }
+}
+
+}  // namespace dtp
+
+extern "C" {
+
+// the single-workgroup forward serves up to kMseMax elements (beyond: the caller's torch path)
+long long dtp_mse_max_elems() { return 1ll << 20; }
+
+int dtp_mse_fwd(const float* a, const float* b, long long n, float* out, void* stream) {
+  if (!a || !b || !out || n <= 0 || n > dtp_mse_max_elems()) return dtp::set_err(-1, "mse_fwd: 1..2^20 elements");
+  hipLaunchKernelGGL(dtp::mse_fwd_kernel, dim3(1), dim3(dtp::kBlock), 0, (hipStream_t)stream, a, b, n,
+                     1.f / (float)n, out);
+  return dtp::check_launch("mse_fwd_kernel");
+}
+
+int dtp_mse_bwd(const float* a, const float* b, const float* g, long long n, float* ga, float* gb, void* stream) {
+  if (!a || !b || !g || n <= 0 || (!ga && !gb)) return dtp::set_err(-1, "mse_bwd: bad arguments");
+  const long long blocks = (n + dtp::kBlock - 1) / dtp::kBlock;
+  const int grid = (int)(blocks < 1024 ? blocks : 1024);
+  hipLaunchKernelGGL(dtp::mse_bwd_kernel, dim3(grid), dim3(dtp::kBlock), 0, (hipStream_t)stream, a, b, g, n,
+                     2.f / (float)n, ga, gb);
+  return dtp::check_launch("mse_bwd_kernel");
+}
+
+}  // extern "C"

@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 from ..data.sampler import BatchIndexer, SamplerGeometry
 from ..data.toy_data import ToyData
+from ..ops.loss import MSELoss
 from ..ops.optim import OptimConfig
 from ..parallel import comm_util
 from ..runtime import bootstrap, checkpoint
@@ -255,7 +256,7 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     rank_print(rank, f"engine: module (FlatDDP over {ddp.comm})")
     from .graph_step import CapturedStep
     opt = FlatOptimizer(bank.flat, bank.flat_grad, _optim(config))
-    lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else torch.nn.MSELoss()
+    lossf = torch.nn.CrossEntropyLoss() if config.loss == "ce" else MSELoss()  # fused drop-in (ops/loss.py)
     start = 0
     if config.resume and config.checkpoint_dir:
         st = checkpoint.load(config.checkpoint_dir)

@@ -12,4 +12,7 @@ for i in 1 2 3 4 5 6; do
   timeout -k 10 150 python3 bench.py --gpus 1 --steps 20 --warmup 5 >> $O/bench_k20.json 2>> $O/err.log || exit $?
 done
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
+# the Trainer's module path with the fused MSE loss: steady samples/s and a kernel trace
+timeout -k 10 300 python3 demo_pytorch_lightning.py --gpus 1 --steps 3000 --seed 0 --root_dir /tmp/ltm --engine module --no_progress > $O/lt_module.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o lt -- python3 demo_pytorch_lightning.py --gpus 1 --steps 3000 --seed 0 --root_dir /tmp/ltq --engine module --no_progress > $O/lt_rocprof.log 2>&1
