@@ -304,4 +304,52 @@ DTP_DEV void lane_kstep(const T& t, f32x4& acc0, f32x4& acc1) {
   else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
 }
 
+#ifndef DTP_LANES_BFMMA
+// 1: bf16 instances run each dW tile as ONE bf16 MFMA over the wave's samples (16x16x16 at
+// 4 lanes per sample: 16 samples; 16x16x32 at 2: 32) instead of TS f32 K = 4 steps
+#define DTP_LANES_BFMMA 1
+#endif
+
+// top halves of two bf16-valued floats as one packed bf16 pair (lo in bits 0..15)
+DTP_DEV unsigned bf_pair(float lo, float hi) {
+  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
+
+// bf16 compute: a whole dW tile of the wave on one bf16 MFMA.  The staged operands hold
+// bf16-rounded floats (Stage::rnd), so packing their top halves is exact.  Reader lane
+// (q, c) holds the K-step operands of samples q, 4 + q, 8 + q, ... (one per f32 K-step);
+// they become its 4 (or 8) K values of the bf16 instruction -- the same sample at the same
+// position for both operands, so the tile sums the same products.
+template <class C, class T>
+DTP_DEV f32x4 lane_tile_bf(const T& t, f32x4 acc) {
+  static_assert(C::TS == 4 || C::TS == 8, "16 or 32 samples per wave");
+  if constexpr (C::TS == 4) {
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    const u2 a = {bf_pair(t.a[0].x, t.a[0].y), bf_pair(t.a[0].z, t.a[0].w)};
+    const u2 b = {bf_pair(t.b[0].x, t.b[0].y), bf_pair(t.b[0].z, t.b[0].w)};
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4, a), __builtin_bit_cast(s4, b), acc, 0, 0, 0);
+  } else {
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 a = {bf_pair(t.a[0].x, t.a[0].y), bf_pair(t.a[0].z, t.a[0].w), bf_pair(t.a[1].x, t.a[1].y),
+                  bf_pair(t.a[1].z, t.a[1].w)};
+    const u4 b = {bf_pair(t.b[0].x, t.b[0].y), bf_pair(t.b[0].z, t.b[0].w), bf_pair(t.b[1].x, t.b[1].y),
+                  bf_pair(t.b[1].z, t.b[1].w)};
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), acc, 0, 0, 0);
+  }
+}
+
+// a whole tile: TS f32 K-steps, or the bf16 instruction (bf16 instances)
+template <class C, class S, class T>
+DTP_DEV f32x4 lane_tile(const T& t, f32x4 acc) {
+  if constexpr (S::BF && DTP_LANES_BFMMA) {
+    return lane_tile_bf<C>(t, acc);
+  } else {
+    f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    static_for<0, C::TS>([&](auto KC) { lane_kstep<decltype(KC)::value>(t, acc, a1); });
+    return acc + a1;
+  }
+}
+
 }  // namespace dtp

@@ -877,9 +877,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       if constexpr (!SC::PACK) {
         __builtin_amdgcn_wave_barrier();
         const auto to = lane_tile_ops<C>(tl, rdoff);
-        f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
-        static_for<0, TS>([&](auto KC) { lane_kstep<decltype(KC)::value>(to, acc[SC::tile(l)], a1); });
-        acc[SC::tile(l)] += a1;
+        acc[SC::tile(l)] = lane_tile<C, S>(to, acc[SC::tile(l)]);
       }
     }
     // hidden layers NL-2 .. 1: block B of layer l in registers, block l-1 prefetched
@@ -910,7 +908,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       LNone none;
       static_for<0, H>([&](auto OC) {
         constexpr int o = decltype(OC)::value;
-        if constexpr (o >= J0) {
+        if constexpr (S::BF && DTP_LANES_BFMMA) {  // the whole tile on one bf16 MFMA
+          if constexpr (o == J0) a0 = lane_tile_bf<C>(to, a0);
+        } else if constexpr (o >= J0) {
           constexpr int k0 = TS * (o - J0) / (H - J0), k1 = TS * (o - J0 + 1) / (H - J0);
           static_for<k0, k1>([&](auto KC) { lane_kstep<decltype(KC)::value>(to, a0, a1); });
         }
@@ -953,9 +953,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       });
       __builtin_amdgcn_wave_barrier();
       const auto to = lane_tile_ops<C>(tl, rdoff);
-      f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
-      static_for<0, TS>([&](auto KC) { lane_kstep<decltype(KC)::value>(to, acc[SC::tile(0)], a1); });
-      acc[SC::tile(0)] += a1;
+      acc[SC::tile(0)] = lane_tile<C, S>(to, acc[SC::tile(0)]);
     }
     DTP_STAMP(8 + wave);
     DTP_STAMP(3);
@@ -964,6 +962,12 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt)
         *reinterpret_cast<f32x4*>(&sm.red[wave][tt * SC::TSZ + SC::tslot(4 * q, col)]) = acc[tt];
+      if constexpr (S::BF && DTP_LANES_BFMMA) {
+        // the bf16 MFMA saw the loss row's per-sample values truncated to bf16: the wave's
+        // loss goes in from a wave sum of the fp32 values instead (same LDS slot, written after)
+        const float lw = wave_sum(p0 ? lpart : 0.f);
+        if (lane == 0) sm.red[wave][SC::losspos()] = lw;
+      }
     }
     __syncthreads();
     const float2 adam_sc = kAdam ? sm.adam_tab[it % kAdamTab] : make_float2(0.f, 1.f);
