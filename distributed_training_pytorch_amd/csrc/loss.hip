@@ -1,3 +1,5 @@
+// Module-path helpers: a fused MSE loss and the Trainer's two-tensor batch gather.
+//
 // Fused MSE loss for the module (autograd) path: what nn.MSELoss(reduction="mean") does
 // in the reference's training step (demo.py:103-104, demo_pytorch_lightning.py:27-33) as
 // ONE launch forward and ONE backward, instead of torch's elementwise square + mean
@@ -47,9 +49,40 @@ __global__ __launch_bounds__(kBlock) void mse_bwd_kernel(const float* __restrict
   }
 }
 
+// the Trainer's replayed batch gather: rows idx of X [nrows, dx] and Y [nrows, dy] into
+// the static batch buffers in ONE launch (torch: one index_select per tensor); indices are
+// clamped into range (an index past the dataset never reads out of bounds)
+__global__ __launch_bounds__(kBlock) void gather_rows2_kernel(const float* __restrict__ X, int dx,
+                                                              const float* __restrict__ Y, int dy,
+                                                              const long long* __restrict__ idx, int n,
+                                                              long long nrows, float* __restrict__ ox,
+                                                              float* __restrict__ oy) {
+  const int w = dx + dy;
+  for (long long t = (long long)blockIdx.x * kBlock + threadIdx.x; t < (long long)n * w;
+       t += (long long)gridDim.x * kBlock) {
+    const int r = (int)(t / w), c = (int)(t - (long long)r * w);
+    long long s = idx[r];
+    s = s < 0 ? 0 : (s >= nrows ? nrows - 1 : s);
+    if (c < dx) ox[(long long)r * dx + c] = X[s * dx + c];
+    else oy[(long long)r * dy + (c - dx)] = Y[s * dy + (c - dx)];
+  }
+}
+
 }  // namespace dtp
 
 extern "C" {
+
+int dtp_gather_rows2(const float* X, int dx, const float* Y, int dy, const long long* idx, int n, long long nrows,
+                     float* ox, float* oy, void* stream) {
+  if (!X || !Y || !idx || !ox || !oy || n <= 0 || dx <= 0 || dy <= 0 || nrows <= 0)
+    return dtp::set_err(-1, "gather_rows2: bad arguments");
+  const long long total = (long long)n * (dx + dy);
+  const long long blocks = (total + dtp::kBlock - 1) / dtp::kBlock;
+  const int grid = (int)(blocks < 1024 ? blocks : 1024);
+  hipLaunchKernelGGL(dtp::gather_rows2_kernel, dim3(grid), dim3(dtp::kBlock), 0, (hipStream_t)stream, X, dx, Y, dy,
+                     idx, n, nrows, ox, oy);
+  return dtp::check_launch("gather_rows2_kernel");
+}
 
 // the single-workgroup forward serves up to kMseMax elements (beyond: the caller's torch path)
 long long dtp_mse_max_elems() { return 1ll << 20; }

@@ -31,6 +31,7 @@ from pathlib import Path
 import torch
 import torch.distributed as dist
 
+from .. import _native as nat
 from ..data.sampler import SamplerGeometry, torch_distributed_indices
 from ..parallel import comm_util
 from ..parallel.ddp import FlatDDP
@@ -118,8 +119,19 @@ class _DevBatch:
         return [self.X[self.sel], self.Y[self.sel]]
 
     def gather_into(self, idx, out):
-        torch.index_select(self.X, 0, idx, out=out[0])
-        torch.index_select(self.Y, 0, idx, out=out[1])
+        X, Y, ox, oy = self.X, self.Y, out[0], out[1]
+        if (X.is_cuda and X.dim() == 2 and Y.dim() == 2 and X.dtype == Y.dtype == ox.dtype == oy.dtype == torch.float32
+                and idx.dtype == torch.int64 and all(t.is_contiguous() for t in (X, Y, idx, ox, oy))
+                and ox.shape == (idx.numel(), X.shape[1]) and oy.shape == (idx.numel(), Y.shape[1])
+                and X.shape[0] == Y.shape[0] and nat.native_enabled()):
+            # both tensors in ONE launch (two index_selects otherwise): each launch costs ~4 us in
+            # the replayed step
+            lib = nat.load()
+            nat.check(lib.dtp_gather_rows2(nat.ptr(X), X.shape[1], nat.ptr(Y), Y.shape[1], nat.ptr(idx), idx.numel(),
+                                           X.shape[0], nat.ptr(ox), nat.ptr(oy), nat.stream_ptr()), "dtp_gather_rows2")
+            return
+        torch.index_select(X, 0, idx, out=ox)
+        torch.index_select(Y, 0, idx, out=oy)
 
 
 _STEADY_AFTER = 10  # batches excluded from Trainer.steady_time
@@ -740,7 +752,8 @@ class Trainer:
                 out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
                     model.training_step(batch, batch_idx)
             loss = out["loss"] if isinstance(out, dict) else out
-            loss.backward()
+            # the seed from a cached tensor of ones (autograd's own would be a fill launch per step)
+            loss.backward(self._backward_seed(loss))
             flat = self._flat_opts[oi] if oi < len(self._flat_opts) else None
             if flat is not None:
                 flat.step()
@@ -749,6 +762,17 @@ class Trainer:
             if len(opts) > 1:
                 model.untoggle_optimizer(oi)
             model._logged[f"train_loss_opt{oi}"] = loss.detach()
+
+    def _backward_seed(self, loss: torch.Tensor):
+        """d loss / d loss for a scalar loss, cached per (dtype, device); None otherwise."""
+        if loss.numel() != 1 or not loss.is_cuda:
+            return None
+        key = (loss.dtype, loss.device, tuple(loss.shape))
+        seeds = self.__dict__.setdefault("_seeds", {})
+        t = seeds.get(key)
+        if t is None:
+            t = seeds[key] = torch.ones_like(loss)
+        return t
 
     def _autocast(self):
         """precision='bf16': torch.autocast around the forward (PL's bf16 plugin); the

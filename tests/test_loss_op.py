@@ -64,3 +64,19 @@ def test_mse_loss_fused_in_a_captured_graph():
         ref.backward()
         torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(w.grad, w2.grad, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_trainer_batch_gather_matches_index_select():
+    """The Trainer's replayed-step gather of (X, Y) rows: one launch, same rows as two
+    index_selects (out-of-range indices clamp instead of faulting)."""
+    from distributed_training_pytorch_amd import _native as nat
+    from distributed_training_pytorch_amd.trainer.trainer import _DevBatch
+
+    nat.require(torch.device("cuda", 0))
+    X = torch.randn(512, 2, device="cuda")
+    Y = torch.randn(512, 1, device="cuda")
+    idx = torch.randperm(512, device="cuda")[:128]
+    out = [torch.empty(128, 2, device="cuda"), torch.empty(128, 1, device="cuda")]
+    _DevBatch(X, Y, idx).gather_into(idx, out)
+    assert torch.equal(out[0], X[idx]) and torch.equal(out[1], Y[idx])
