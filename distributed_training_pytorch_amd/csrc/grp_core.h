@@ -491,14 +491,14 @@ DTP_DEV float grp_allreduce_split(const GrpCtx& c, int model, float (&g)[NPT], f
 // gather and index request), run exactly once by every thread while its memory requests are
 // in flight: the publisher after its stores, a poller between its first poll's issue and
 // its consumption.
-template <int P, int NPT, int NTHREADS, class OverlapFn>
-DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
-                                   bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain, GrpProf* prof,
-                                   OverlapFn ov) {
-  constexpr int NG = grp_ng3(P), PS = grp_ps3(P);
+template <int P, int NPT, int NTHREADS, int NG, class OverlapFn>
+DTP_DEV float grp_allreduce_split3_ng(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                                      bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain, GrpProf* prof,
+                                      OverlapFn ov) {
+  constexpr int NGF = grp_ng3(P), PS = grp_ps3(P);
   constexpr int NPOLL = NTHREADS - kWave;  // poller lanes (waves 1..)
   constexpr int slot = grp_slot16(P, NPT);
-  static_assert(NG <= slot, "a member's 3-float granules fit its slot of the exchange buffer");
+  static_assert(NGF <= slot, "a member's 3-float granules fit its slot of the exchange buffer");
   static_assert(NTHREADS > kWave, "one publisher wave and at least one poller wave");
   float* const pub = lds;
   float* const peer = lds + PS;  // peer[r * PS + i]: member r's float i
@@ -511,7 +511,7 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
     pub[P] = loss;
     pub[P + 1] = __uint_as_float(xcc);
 #pragma unroll
-    for (int i = P + 2; i < 3 * NG; ++i) pub[i] = 0.f;
+    for (int i = P + 2; i < 3 * NGF; ++i) pub[i] = 0.f;
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(c.buf);
@@ -638,7 +638,7 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
         }
       }
     };
-    constexpr int MAXI = ((kGrpMax - 1) * NG + NPOLL - 1) / NPOLL;
+    constexpr int MAXI = ((kGrpMax - 1) * NGF + NPOLL - 1) / NPOLL;
     const int pi = (total + NPOLL - 1) / NPOLL;
     if (pi <= 1) run(std::integral_constant<int, 1>{});
     else if (pi <= 2) run(std::integral_constant<int, 2>{});
@@ -672,6 +672,26 @@ DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], 
 #pragma unroll
   for (int k = 0; k < NPT; ++k) g[k] = acc[k];
   return lacc;
+}
+
+#ifndef DTP_GRP_SHORT
+// 1: drop the XCC id from the payload once plain (grp_allreduce_split3).  Measured slower
+// (toy 3.43 vs 3.35, CE head 3.96 vs 3.93 us/step, profiles/r5_exchange/short/): a second
+// instance of the exchange costs more than the granule it saves
+#define DTP_GRP_SHORT 0
+#endif
+
+// NG granules per member: the full payload (gradients, loss, XCC id) until every member is
+// known to share this XCD (plain), then without the XCC id, which has done its job: (P + 1)
+// floats (the CE head's 383 gradients + loss: 128 granules, 2 poll items per lane instead of 3)
+template <int P, int NPT, int NTHREADS, class OverlapFn>
+DTP_DEV float grp_allreduce_split3(const GrpCtx& c, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                                   bool& dead, float* __restrict__ lds, unsigned xcc, bool& plain, GrpProf* prof,
+                                   OverlapFn ov) {
+  constexpr int NGF = grp_ng3(P), NGS = (P + 1 + 2) / 3;
+  if (DTP_GRP_SAME_XCD && DTP_GRP_SHORT && NGS < NGF && plain)
+    return grp_allreduce_split3_ng<P, NPT, NTHREADS, NGS>(c, model, g, loss, epoch, tid, dead, lds, xcc, plain, prof, ov);
+  return grp_allreduce_split3_ng<P, NPT, NTHREADS, NGF>(c, model, g, loss, epoch, tid, dead, lds, xcc, plain, prof, ov);
 }
 
 #ifndef DTP_GRP_DIRECT3
