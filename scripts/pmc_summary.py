@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-wave, per-step SQ counters of the fused step from `scripts/pmc_step.sh` runs.
 
-Usage: python scripts/pmc_summary.py TAG [TAG ...]   (reads gpurun_out/pmc_TAG/{A,B}/)
-The last mlp_train_kernel dispatch of each pass is the 1000-step persistent launch
-of bench.py; its counters are divided by 1000 steps and 8 waves (2 workgroups x 4).
+Usage: python scripts/pmc_summary.py [--waves N] TAG [TAG ...]   (reads gpurun_out/pmc_TAG/{A,B}/)
+The last fused-step dispatch (mlp_train_kernel / mlp_train_lanes_kernel) of each pass is the
+1000-step persistent launch of bench.py; its counters are divided by 1000 steps and the
+waves of the launch (8: one workgroup per model; 32: the split-batch step, 8 workgroups).
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* are in quad-cycles.
 """
 import collections
@@ -18,7 +19,7 @@ def summary(tag: str, base: str = "gpurun_out", steps: int = 1000, waves: int = 
     res = {}
     for p in "AB":
         path = os.path.join(ROOT, base, f"pmc_{tag}", p, f"{p}_counter_collection.csv")
-        rows = [r for r in csv.DictReader(open(path)) if "mlp_train_kernel" in r["Kernel_Name"]]
+        rows = [r for r in csv.DictReader(open(path)) if "mlp_train" in r["Kernel_Name"]]
         by = collections.defaultdict(dict)
         for r in rows:
             by[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
@@ -27,5 +28,11 @@ def summary(tag: str, base: str = "gpurun_out", steps: int = 1000, waves: int = 
 
 
 if __name__ == "__main__":
-    for t in sys.argv[1:]:
-        print(t, summary(t))
+    args = sys.argv[1:]
+    w = 8
+    if "--waves" in args:
+        i = args.index("--waves")
+        w = int(args[i + 1])
+        args = args[:i] + args[i + 2:]
+    for t in args:
+        print(t, summary(t, waves=w))

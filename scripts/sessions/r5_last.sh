@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 5, last validation: K=2000 and the driver's K=20 line (fresh processes), smoke, the
+# whole GPU suite, a rocprofv3 kernel-trace/stats run of the bench and two SQ counter passes
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r5last
+mkdir -p $O
+for i in 1 2; do
+  timeout -k 10 150 python bench.py --steps 2000 --warmup 200 >> $O/bench_default.json 2>> $O/err.log || exit $?
+done
+for i in 1 2 3 4 5 6; do
+  timeout -k 10 150 python3 bench.py --gpus 1 --steps 20 --warmup 5 >> $O/bench_k20.json 2>> $O/err.log || exit $?
+done
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --steps 2000 --warmup 200 > $O/rocprof.log 2>&1 || exit $?
+bash scripts/pmc_step.sh r5last > $O/pmc.log 2>&1
