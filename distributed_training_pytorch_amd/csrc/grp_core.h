@@ -98,6 +98,13 @@ DTP_HD constexpr int grp_slot16(int P, int npt) { return xgmi_slot16(P, npt); }
 // (profiles/r5_exchange/overlap/) -- the wait counts around the polls lose their slack
 #define DTP_GRP_OVERLAP 0
 #endif
+#ifndef DTP_GRP_ZERO_MISSING
+// 1: a timed-out exchange's missing items add +0 (grp_allreduce_split3) instead of what an
+// earlier exchange left in their LDS rows.  Off: the code on the pollers' path alone cost
+// 3.42 vs 3.36 us/step (profiles/r5_exchange/zero_missing/); a timeout already marks the run
+// failed through the status word (check_comm raises), whatever the values
+#define DTP_GRP_ZERO_MISSING 0
+#endif
 #ifndef DTP_GRP_PIPE3
 // the 3-float form's pollers: 0 = one poll in flight, 1 = two.  With 2 items per lane one poll
 // measured faster (3.40 vs 3.44-3.46 us/step, profiles/r5_exchange/g3/); the 2-float form
@@ -599,6 +606,17 @@ DTP_DEV float grp_allreduce_split3_ng(const GrpCtx& c, int model, float (&g)[NPT
           }
         }
       };
+      // a timed-out (or already dead) exchange: the items still missing add +0, not the
+      // values an earlier exchange left in the LDS rows (the status word reports the timeout)
+      auto zero_missing = [&]() {
+#pragma unroll
+        for (int j = 0; j < PI; ++j) {
+          if ((pending >> j) & 1u) {
+            float* d = peer + dst[j];
+            d[0] = d[1] = d[2] = 0.f;
+          }
+        }
+      };
       u32x4 xa[PI], xb[PI];
       bool ovd = !DTP_GRP_OVERLAP;
       if (!DTP_GRP_PIPE3) {  // one poll in flight (the default with 3-float granules)
@@ -613,6 +631,7 @@ DTP_DEV float grp_allreduce_split3_ng(const GrpCtx& c, int model, float (&g)[NPT
           if (pending && expired()) dead = true;
         }
         if (!ovd) ov();
+        if (DTP_GRP_ZERO_MISSING && pending) zero_missing();
         return;
       }
       if (pending && !dead) issue(xa);
@@ -637,6 +656,7 @@ DTP_DEV float grp_allreduce_split3_ng(const GrpCtx& c, int model, float (&g)[NPT
           break;
         }
       }
+      if (DTP_GRP_ZERO_MISSING && pending) zero_missing();
     };
     constexpr int MAXI = ((kGrpMax - 1) * NGF + NPOLL - 1) / NPOLL;
     const int pi = (total + NPOLL - 1) / NPOLL;
