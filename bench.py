@@ -193,6 +193,12 @@ def self_launch(a, argv: list[str]) -> int:
 
 def main():
     a = parse()
+    # the collective environment goes in FIRST: HSA reads HSA_ENABLE_IPC_MODE_LEGACY once,
+    # at the process's first GPU touch (set_wait_mode below is one), and the self-launched
+    # ranks inherit it from this process's environment.  Set later, the IPC mapping of the
+    # in-kernel exchange fails and the run measures the RCCL fallback instead.
+    ipc_env_at_start = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+    bootstrap.configure_collective_env()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and os.environ.get("DTP_BENCH_CHILD") != "1":
         sys.exit(self_launch(a, sys.argv[1:]))
     if torch.cuda.device_count() > 0:  # counting devices does not initialise the GPU
@@ -205,7 +211,6 @@ def main():
         _native.set_wait_mode(os.environ.get("DTP_WAIT_MODE", "spin"))
     # the demos' launch path (runtime/bootstrap.py): torchrun / SLURM / MPI env
     # discovery, device binding, process-group init
-    bootstrap.configure_collective_env()
     env = bootstrap.detect()
     ndev = torch.cuda.device_count()
     if a.share_gpu and ndev > 0:
@@ -322,6 +327,9 @@ def main():
     value = total_samples / elapsed
     diag = {"extra_ms_per_step": extra} if extra else {}
     if world > 1 and a.impl == "native":
+        if runner.comm != "xgmi" and rank == 0:
+            sys.stderr.write(f"[bench] W={world}: in-kernel xGMI exchange NOT used (comm={runner.comm}): "
+                             f"{runner.comm_fallback_reason}\n")
         # where a multi-GPU step goes (readable from the JSON line alone): the in-kernel
         # exchange's wait (publish -> last peer granule, per rank) and the rest of the step
         diag["comm_fallback_reason"] = runner.comm_fallback_reason
@@ -378,6 +386,9 @@ def main():
                 "parallelism": f"dp{world}",
                 "impl": a.impl,
                 "dataset_samples": n,
+                # the IPC-mode variable as this rank's process found it at start (self-launched
+                # ranks inherit it from the parent, which sets it before the launch)
+                "ipc_env_at_start": ipc_env_at_start,
                 **cfg_desc,
             },
             "final_loss": final_loss,

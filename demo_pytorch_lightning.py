@@ -19,6 +19,7 @@ import torch.nn as nn  # noqa: E402
 from torch.utils.data import DataLoader  # noqa: E402
 
 from distributed_training_pytorch_amd.ops.loss import MSELoss  # noqa: E402
+from distributed_training_pytorch_amd.runtime import bootstrap  # noqa: E402
 from distributed_training_pytorch_amd.runtime.errors import record  # noqa: E402
 from distributed_training_pytorch_amd.trainer import LightningModule, Trainer  # noqa: E402
 from toy_model_and_data import ToyData, ToyModel  # noqa: E402
@@ -86,6 +87,8 @@ def get_args(argv=None):
 @record
 def main(argv=None):
     a = get_args(argv)
+    # before the first GPU touch (torch.cuda.is_available below): HSA reads the IPC mode once
+    bootstrap.configure_collective_env()
     torch.manual_seed(a.seed)
     ds = ToyData(seed=a.seed)
     dl = DataLoader(ds, batch_size=a.batch_size, pin_memory=torch.cuda.is_available(), num_workers=a.num_workers)

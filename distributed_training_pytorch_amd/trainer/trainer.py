@@ -239,13 +239,13 @@ class Trainer:
 
     # ------------------------------------------------------------------ distributed
     def _setup(self):
+        bootstrap.configure_collective_env()  # before bind_device: HSA reads the IPC mode at its first touch
         env = bootstrap.detect()
         device = torch.device("cpu")
         if self.accelerator == "gpu" and torch.cuda.is_available():
             device = bootstrap.bind_device(env, "cuda")
         if self.strategy in ("ddp", "ddp_spawn", "ddp_find_unused_parameters_false") or env.world_size > 1:
             backend = os.environ.get("PL_TORCH_DISTRIBUTED_BACKEND", "nccl" if device.type == "cuda" else "gloo")
-            bootstrap.configure_collective_env()
             bootstrap.init_process_group(env, backend, device, datetime.timedelta(minutes=60))
         self.env = env
         self.device = device

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _env(**kw):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
-                        "DTP_BENCH_CHILD")}
+                        "DTP_BENCH_CHILD", "HSA_ENABLE_IPC_MODE_LEGACY")}
     env["HIP_VISIBLE_DEVICES"] = ""  # CPU ranks even on a GPU box
     env["CUDA_VISIBLE_DEVICES"] = ""
     env.update(kw)
@@ -41,3 +41,14 @@ def test_bench_self_launch_fails_with_a_rank():
     assert r.returncode != 0
     assert "forced failure" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_children_inherit_ipc_env():
+    """The parent sets the collective environment before it launches the ranks: a rank
+    finds HSA_ENABLE_IPC_MODE_LEGACY=0 at its own start, although the caller's
+    environment (like the driver's) never set it.  HSA reads it once, at the first GPU
+    touch, so a rank that set it itself later would be too late."""
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.strip()][0])
+    assert rec["config"]["ipc_env_at_start"] == "0", rec["config"]

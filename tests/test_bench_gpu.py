@@ -109,15 +109,20 @@ def test_bench_strong_scaling_share_gpu(world):
 
 def test_bench_self_launch_share_gpu():
     """No torchrun around bench.py: --gpus 2 starts its own two ranks (the driver's N-GPU
-    call shape), here both on the one GPU."""
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
-                                                             "MASTER_PORT", "LOCAL_WORLD_SIZE")}
-    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    call shape), here both on the one GPU -- from an environment WITHOUT
+    HSA_ENABLE_IPC_MODE_LEGACY, as the driver may call it: bench.py must set it itself
+    before any GPU touch, or the IPC mapping fails and the run falls back to RCCL."""
+    drop = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
+            "HSA_ENABLE_IPC_MODE_LEGACY", "DTP_BENCH_CHILD")
+    env = {k: v for k, v in os.environ.items() if k not in drop}
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu", "--steps", "20", "--warmup", "5"],
                        cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
-    assert rec["n_gpus"] == 2 and rec["config"]["comm"] == "xgmi" and rec["value"] > 0
+    assert rec["n_gpus"] == 2 and rec["value"] > 0
+    assert rec["config"]["comm"] == "xgmi", (rec["config"], rec.get("comm_fallback_reason"))
+    assert rec["comm_fallback_reason"] is None
+    assert rec["config"]["ipc_env_at_start"] == "0"
 
 
 def test_bench_weak_scaling_flag_share_gpu():
