@@ -321,6 +321,11 @@ def main():
         sync_barrier()
         extra.append(round(1e3 * (time.perf_counter() - u0) / a.steps, 5))
     gc.enable()
+    if a.impl == "native":  # the instance the run actually launched (the engine exists now)
+        cfg_desc.update(lanes_per_sample=runner.lanes, waves_per_cu=runner.kernel_waves,
+                        workgroups_per_model=runner.groups)
+        if runner.groups_refused:
+            cfg_desc["groups_refused"] = runner.groups_refused
     elapsed = comm_util.all_reduce_scalar(t1 - t0, dist.ReduceOp.MAX)
     ms_per_step = 1e3 * elapsed / a.steps
     total_samples = comm_util.all_reduce_scalar(float(per_rank_batch * a.steps))

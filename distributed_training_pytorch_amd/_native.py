@@ -141,6 +141,7 @@ class SplitStageArgs(ctypes.Structure):
         ("link_local", c_int),
         ("smp", SamplerCfg),
         ("hp", Hyper),
+        ("grp_buf", c_void_p),
     ]
 
 
@@ -152,7 +153,7 @@ class SplitLaunch(ctypes.Structure):
         ("stage", SplitStageArgs * SPLIT_MAX_LOCAL),
         ("shape_id", c_int * SPLIT_MAX_LOCAL),
         ("n", c_int),
-        ("pad_", c_int),
+        ("members", c_int),
     ]
 
 
@@ -255,6 +256,9 @@ def _declare(lib):
         "dtp_split_shape_id": (c_int, [c_int] * 6),
         "dtp_split_stage_supported": (c_int, [c_int] * 6),
         "dtp_split_link_bytes": (c_longlong, [c_int, c_int]),
+        "dtp_split_lanes_launch": (c_int, [P(SplitLaunch), c_void_p]),
+        "dtp_split_lanes_supported": (c_int, [c_int] * 6),
+        "dtp_split_lanes_grp_bytes": (c_longlong, [c_int, c_int]),
         "dtp_sampler_indices": (c_int, [P(SamplerCfg), c_longlong, c_int, c_void_p, c_void_p]),
         "dtp_get_device": (c_int, [P(c_int)]),
         "dtp_device_count": (c_int, [P(c_int)]),
@@ -435,6 +439,9 @@ def native_enabled() -> bool:
 # (its static destructors, after Python has gone) was the suspect of an exit-time
 # SIGSEGV in __cxa_finalize under rocprofv3 (profiles/r4_split_streams/README.md)
 _owned_streams: list = []
+# CU count of every stream made by cu_masked_stream (raw handle -> CUs): a kernel whose
+# workgroups must all be resident at once (the split-batch step) checks it
+masked_stream_cus: dict[int, int] = {}
 _atexit_registered = False
 
 
@@ -455,6 +462,7 @@ def destroy_owned_streams() -> None:
         return
     while _owned_streams:
         h, dev = _owned_streams.pop()
+        masked_stream_cus.pop(h, None)
         try:
             with torch.cuda.device(dev):
                 _lib.dtp_stream_destroy(ctypes.c_void_p(h))
@@ -496,4 +504,5 @@ def cu_masked_stream(device, cus) -> "torch.cuda.ExternalStream":
     out = ctypes.c_void_p()
     check(lib.dtp_stream_create_cu_mask(mask, words, ctypes.byref(out)), "dtp_stream_create_cu_mask")
     _own_stream(out.value, torch.device(device))
+    masked_stream_cus[out.value] = len(cus)
     return torch.cuda.ExternalStream(out.value, device=torch.device(device))

@@ -54,13 +54,16 @@ constexpr int kWaves = kBlock / kWave;
 // entries base + tid + j * kBlock (j < J) of the host's Adam table for a launch starting
 // at step t0: {lr / (1 - b1^t1), sqrt(1 - b2^t1)} with t1 = t0 + e + 1, clamped to the
 // table's saturated last row
+// (only the rows the launch's n_steps reach: a 20-step launch loads 20 entries, not 1024)
 template <int J, int NTH = kBlock>
 DTP_DEV void adam_tab_load(const DtpTrainArgs& a, int t0, int base, int tid, float2 (&v)[J]) {
   const float2* __restrict__ tab = reinterpret_cast<const float2*>(a.adam_tab);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const long long t1 = (long long)t0 + base + tid + j * NTH + 1;
-    v[j] = tab[t1 < a.adam_tab_len ? t1 : a.adam_tab_len - 1];
+    const int e = base + tid + j * NTH;
+    const long long t1 = (long long)t0 + e + 1;
+    v[j] = make_float2(0.f, 1.f);
+    if (e < a.n_steps) v[j] = tab[t1 < a.adam_tab_len ? t1 : a.adam_tab_len - 1];
   }
 }
 template <int J, int NTH = kBlock>
@@ -585,8 +588,10 @@ struct LaneSmem {
   // split-batch exchange (grp_allreduce_split): this member's payloads, then every member's
   static constexpr int GSLOT = xgmi_slot16(S::P, (S::P + 64 * NW - 1) / (64 * NW));
   // (the 3-float form, DTP_GRP_G3: (kGrpMax + 1) rows of grp_ps3(P) floats)
-  static constexpr int GX2 = (kGrpMax + 1) * GSLOT > (kGrpMax + 1) * grp_ps3(S::P) / 2
-                                 ? (kGrpMax + 1) * GSLOT : (kGrpMax + 1) * grp_ps3(S::P) / 2;
+  // (the 3-float xGMI form, DTP_XGMI_G3: xgmi_g3_lds_floats(P) floats)
+  static constexpr int GX2a = (kGrpMax + 1) * GSLOT > (kGrpMax + 1) * grp_ps3(S::P) / 2
+                                  ? (kGrpMax + 1) * GSLOT : (kGrpMax + 1) * grp_ps3(S::P) / 2;
+  static constexpr int GX2 = GX2a > xgmi_g3_lds_floats(S::P) / 2 ? GX2a : xgmi_g3_lds_floats(S::P) / 2;
   alignas(16) float2 gx[GRP ? GX2 : 2];
 };
 
@@ -615,7 +620,9 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   // the split exchanges' LDS: the split-batch step, and the xGMI instances of 4 waves (the
   // 8-wave ones keep the single-role exchange: their LDS is full)
   constexpr bool kXsplit = DTP_XGMI_SPLIT && NW == 4 && (MODE == DTP_MODE_XGMI_ADAM || MODE == DTP_MODE_XGMI_SGD);
-  __shared__ __align__(16) LaneSmem<S, L, NW, GRP || kXsplit> sm;
+  // the 3-float cross-GPU exchange (xgmi_core.h:xgmi_allreduce_g3), 4-wave instances
+  constexpr bool kXg3 = DTP_XGMI_G3 && !kXsplit && NW == 4 && kXgmi;
+  __shared__ __align__(16) LaneSmem<S, L, NW, GRP || kXsplit || kXg3> sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int model = GRP ? (int)(blockIdx.x & 7u) : (int)blockIdx.x;
   const int gk = GRP ? (int)(blockIdx.x >> 3) : 0;  // member of the model's group
@@ -637,6 +644,21 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   }
   unsigned long long* prof = reinterpret_cast<unsigned long long*>(a.status);
   const float slope = a.hp.slope;
+  // PROF: launch-level stamps in row 0 of this block (thread 0): 20 entry, 18 prologue LDS
+  // fills issued, 19 first barrier (global loads consumed), 22 weight scatter, 23 Adam table,
+  // 29 loop start, 24 loop end, 21 write-back issued (the lead)
+  auto stamp_launch = [&](int slot) {
+    if constexpr (PROF) {
+      if (tid == 0) {
+        unsigned long long t_;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        prof[(size_t)blockIdx.x * 8 * 32 + slot] = t_;
+      }
+    }
+  };
+  stamp_launch(20);
 
   // ---- prologue (all global reads issued before the first wait, as in mlp_train_kernel)
   float* __restrict__ gp = a.params + (size_t)model * P;
@@ -716,6 +738,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
   for (int e = tid; e < smp.n * YD; e += NTH) sm.data[smp.n * S::IN + e] = a.Y[e];
   const int yoff = smp.n * S::IN;
+  stamp_launch(18);
   // this wave's staging areas: zero (unwritten rows / columns stay finite), then the
   // constant-1 bias columns of every tile, written once per launch
   {
@@ -729,6 +752,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     });
   }
   __syncthreads();  // weight blocks zeroed (pads stay 0) before the owners scatter into them
+  stamp_launch(19);
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     if (NPT * tid + k < P) {
@@ -737,6 +761,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       if (pb[k] >= 0) sm.wb[pb[k]] = wv;
     }
   }
+  stamp_launch(22);
   int lslot = a.loss_log ? t0 % a.loss_log_cap : 0;
   auto fast_gather = [&](int di, float (&x)[S::IN], float (&y)[S::OUT]) {
     const bool v = di >= 0;
@@ -770,6 +795,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     }
   };
   if (kAdam) fill_adam(0);
+  stamp_launch(23);
   // per-lane LDS bases: the part's slice of the partitioned blocks, the sample's slot in a
   // staged operand (+ the part's first column), the MFMA reader's operands
   const float* const wlp = sm.wb + part * C::NOP;
@@ -791,6 +817,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   };
   const bool p0 = part == 0;
   __syncthreads();
+  stamp_launch(29);
 
   for (int it = 0; it < a.n_steps; ++it) {
     DTP_STAMP(0);
@@ -1069,7 +1096,11 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     float gloss = mean_loss;
     if constexpr (kXgmi) {
       xepoch += 1u;
-      if constexpr (kXsplit) {
+      if constexpr (kXg3) {
+        const XgmiCtx xc{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
+        gloss = xgmi_allreduce_g3<P, NPT, NTH>(xc, model, g, mean_loss, xepoch, tid, reinterpret_cast<float*>(sm.gx),
+                                               xdead, DTP_XWAIT ? xwait : nullptr, GRP ? a.groups : 1, gk);
+      } else if constexpr (kXsplit) {
         const XgmiCtx xc{a.peers, a.status, a.smp.world, a.smp.rank, a.n_models, a.timeout_us};
         gloss = xgmi_allreduce_split<P, NPT, NTH>(xc, model, g, mean_loss, xepoch, tid, sm.gx,
                                                   sm.gx + xgmi_slot16(P, NPT), xdead, DTP_XWAIT ? xwait : nullptr,
@@ -1113,6 +1144,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     DTP_STAMP(7);
   }
 
+  stamp_launch(24);
   if (!lead) return;  // every member holds the same state: the first writes it back
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -1127,6 +1159,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   if (kXgmi && tid == 0) a.epoch[model] = xepoch;
   if (GRP && !kXgmi && tid == 0) a.grp_epoch[model] = xepoch;
   if (DTP_XWAIT && kXgmi && model == 0 && a.status) xgmi_record_wait(a.status, xwait, (unsigned long long)a.n_steps, tid);
+  stamp_launch(21);
 }
 
 // ------------------------------------------------------------------------------

@@ -399,6 +399,187 @@ DTP_DEV float xgmi_allreduce_split(const XgmiCtx& a, int model, float (&g)[NPT],
   return acc[GPT][0];
 }
 
+#ifndef DTP_XGMI_G3
+// 1: the several-lanes steps (4 waves) run the cross-GPU exchange on 3-float granules with a
+// destination-dealt publish (xgmi_allreduce_g3); 0: the 2-float owner-thread form above
+#define DTP_XGMI_G3 1
+#endif
+#ifndef DTP_XGMI_G3_PUBW
+// xgmi_allreduce_g3 roles: 0 = every wave publishes its dealt destinations, then polls;
+// n > 0 = waves 0..n-1 publish every destination, the other waves poll
+#define DTP_XGMI_G3_PUBW 0
+#endif
+#ifndef DTP_XGMI_G3_SLEEP
+#define DTP_XGMI_G3_SLEEP 0  // s_sleep units between two polls of xgmi_allreduce_g3 (0: none)
+#endif
+
+// 3-float granules of a member's cross-GPU payload: the P gradients and the loss
+DTP_HD constexpr int xgmi_ng3(int P) { return (P + 1 + 2) / 3; }
+// LDS floats per member row of xgmi_allreduce_g3 (a float4 multiple)
+DTP_HD constexpr int xgmi_ps3(int P) { return (3 * xgmi_ng3(P) + 3) & ~3; }
+// LDS floats of xgmi_allreduce_g3: this member's row, then one row per virtual member
+DTP_HD constexpr int xgmi_g3_lds_floats(int P) { return (1 + kXgmiMaxWorld) * xgmi_ps3(P); }
+
+// Tag of a 3-float cross-GPU granule {epoch ^ h(v0, v1, v2), v0, v1, v2}: nonlinear in the
+// payload (two hash32 rounds), so a granule torn across an xGMI link -- new and old halves
+// of a slot two exchanges apart -- passes only on a 2^-32 collision.
+DTP_DEV uint32_t xgmi_hash3(uint32_t a, uint32_t b, uint32_t c) {
+  return hash32(a ^ hash32(b ^ ((c << 13) | (c >> 19)) ^ 0x9E3779B9u));
+}
+
+// The cross-GPU all-reduce on 3-float granules (round 6; the on-chip split exchange's form,
+// grp_core.h:grp_allreduce_split3, carried to the system scope):
+//   * the owners stage the member's payload in LDS as one flat row (gradients 0..P-1, the
+//     loss at P); granule q = floats [3q, 3q + 3) as {epoch ^ xgmi_hash3(v), v}: 124 granules
+//     for the toy model instead of 187 two-float ones;
+//   * publish: the destination ranks (every rank with a reader of this slot -- the own
+//     rank too when other local members read it, GR > 1) are dealt to the waves, d-th
+//     destination to wave d % NPW; a wave stores all NG granules of its destination
+//     (2 coalesced 16-byte stores per lane, a wave-uniform buffer resource), so no lane
+//     issues more than 2 ceil(D / NPW) stores (W = 8: 4, was 7 per owner thread);
+//   * poll: items (virtual member v != R, granule q) spread over the poller lanes (W = 8:
+//     <= 4 per lane), every still-missing item re-requested each round, accepted granules
+//     parked in LDS;
+//   * one barrier, then every thread sums its parameters over the slots in order 0..V-1
+//     (its own value from registers): the same bits on every rank, and the same bits as
+//     xgmi_allreduce_slots (identical add order).
+// lds: xgmi_g3_lds_floats(P) floats.  Spins bounded (status word, dead flag), as above.
+template <int P, int NPT, int NTHREADS>
+DTP_DEV float xgmi_allreduce_g3(const XgmiCtx& a, int model, float (&g)[NPT], float loss, unsigned epoch, int tid,
+                                float* __restrict__ lds, bool& dead, unsigned long long* waited = nullptr, int GR = 1,
+                                int gk = 0) {
+  constexpr int NG = xgmi_ng3(P), PS = xgmi_ps3(P);
+  constexpr int NW = NTHREADS / kWave;
+  constexpr int NPW = DTP_XGMI_G3_PUBW > 0 ? DTP_XGMI_G3_PUBW : NW;  // publisher waves
+  constexpr int NPOLL = DTP_XGMI_G3_PUBW > 0 ? NTHREADS - kWave * DTP_XGMI_G3_PUBW : NTHREADS;
+  constexpr int P0 = DTP_XGMI_G3_PUBW > 0 ? kWave * DTP_XGMI_G3_PUBW : 0;  // first poller lane
+  constexpr int slot = xgmi_slot16(P, NPT);
+  constexpr int MAXJ = (NG + kWave - 1) / kWave;  // granules per publisher lane and destination
+  static_assert(NG <= slot, "a member's 3-float granules fit its slot of the receive buffer");
+  static_assert(NPW <= NW && NPOLL >= kWave, "publisher and poller waves");
+  float* const pub = lds;
+  float* const peer = lds + PS;  // peer[v * PS + i]: virtual member v's float i
+  const int V = a.world * GR, R = a.rank * GR + gk;
+  const size_t base = (size_t)((int)(epoch & 1u) * a.n_models + model) * V;
+  const int wave = tid / kWave, lane = tid - (tid / kWave) * kWave;
+  // 1. the payload into LDS
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (NPT * tid + k < P) pub[NPT * tid + k] = g[k];
+  if (tid == 0) {
+    pub[P] = loss;
+#pragma unroll
+    for (int i = P + 1; i < 3 * NG; ++i) pub[i] = 0.f;
+  }
+  __syncthreads();
+  const unsigned long long t_pub0 = waited ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // 2. publish: this wave's dealt destinations (the ranks other than this one first, in
+  // ring order from rank + 1, then this rank's own buffer when GR > 1)
+  if (wave < NPW) {
+    u32x4 gq[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int q = lane + j * kWave < NG ? lane + j * kWave : NG - 1;
+      const uint32_t x0 = __float_as_uint(pub[3 * q]), x1 = __float_as_uint(pub[3 * q + 1]),
+                     x2 = __float_as_uint(pub[3 * q + 2]);
+      gq[j] = u32x4{epoch ^ xgmi_hash3(x0, x1, x2), x0, x1, x2};
+    }
+    const int D = GR > 1 ? a.world : a.world - 1;
+    for (int di = wave; di < D; di += NPW) {
+      int d = a.rank + 1 + di;
+      d = d >= a.world ? d - a.world : d;  // di = world - 1 (GR > 1 only): this rank
+      const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(a.peers[d]);
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        const int q = lane + j * kWave;
+        if (q < NG)
+          __builtin_amdgcn_raw_buffer_store_b128(gq[j], rs, (int)(((base + R) * slot + q) * 16), 0, kSysCoherent);
+      }
+    }
+  }
+  const unsigned long long t_pub = waited ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  if (waited && wave < NPW) waited[1] += t_pub - t_pub0;
+  // 3. poll the other V - 1 slots of the local buffer
+  if (tid >= P0) {
+    const __amdgpu_buffer_rsrc_t ms = xgmi_rsrc(a.peers[a.rank]);
+    const int pl = tid - P0;
+    const int total = (V - 1) * NG;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long deadline = t0 + (unsigned long long)(a.timeout_us > 0 ? a.timeout_us : 2000000) * 100ull;
+    unsigned spins = 0;
+    auto run = [&](auto PIC) {
+      constexpr int PI = decltype(PIC)::value;
+      int off[PI], dst[PI];
+      uint32_t pending = 0u;
+#pragma unroll
+      for (int j = 0; j < PI; ++j) {
+        const int i = pl + j * NPOLL;
+        const int vi = i / NG, q = i - vi * NG;
+        const int v = vi < R ? vi : vi + 1;
+        const bool in = i < total;
+        off[j] = in ? (int)(((base + v) * slot + q) * 16) : 0;
+        dst[j] = v * PS + 3 * q;
+        if (in) pending |= 1u << j;
+      }
+      while (pending && !dead) {
+        u32x4 x[PI];
+        asm volatile("" ::: "memory");  // a poll is never merged with, or hoisted above, an earlier one
+#pragma unroll
+        for (int j = 0; j < PI; ++j) x[j] = __builtin_amdgcn_raw_buffer_load_b128(ms, off[j], 0, kSysCoherent);
+#pragma unroll
+        for (int j = 0; j < PI; ++j) {
+          if (((pending >> j) & 1u) && (x[j].x ^ xgmi_hash3(x[j].y, x[j].z, x[j].w)) == epoch) {
+            float* d = peer + dst[j];
+            d[0] = __uint_as_float(x[j].y);
+            d[1] = __uint_as_float(x[j].z);
+            d[2] = __uint_as_float(x[j].w);
+            pending &= ~(1u << j);
+          }
+        }
+        if (!pending) break;
+        if ((++spins & 15u) == 0u && __builtin_amdgcn_s_memrealtime() > deadline) {
+          if (a.status) {
+            atomicExch(&a.status[0], 1);
+            atomicExch(&a.status[1], (int)epoch);
+          }
+          dead = true;
+        }
+        if (DTP_XGMI_G3_SLEEP > 0) __builtin_amdgcn_s_sleep(DTP_XGMI_G3_SLEEP);
+      }
+      // a timed-out exchange adds +0 for what never arrived (not an earlier exchange's rows)
+      if (pending) {
+#pragma unroll
+        for (int j = 0; j < PI; ++j)
+          if ((pending >> j) & 1u) peer[dst[j]] = peer[dst[j] + 1] = peer[dst[j] + 2] = 0.f;
+      }
+    };
+    constexpr int MAXI = ((kXgmiMaxWorld - 1) * NG + NPOLL - 1) / NPOLL;
+    static_assert(MAXI <= 32, "pending mask");
+    const int pi = (total + NPOLL - 1) / NPOLL;
+    if (pi <= 1) run(std::integral_constant<int, 1>{});
+    else if (pi <= 2) run(std::integral_constant<int, 2>{});
+    else if (pi <= 4) run(std::integral_constant<int, 4 < MAXI ? 4 : MAXI>{});
+    else run(std::integral_constant<int, MAXI>{});
+    if (waited) waited[0] += __builtin_amdgcn_s_memrealtime() - t0;
+  }
+  __syncthreads();
+  // 4. slot-order sums (a dead exchange's rows hold +0 where nothing arrived)
+  float acc[NPT], lacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) acc[k] = 0.f;
+  const int p0 = NPT * tid < P ? NPT * tid : 0;
+  for (int v = 0; v < V; ++v) {
+    const float* row = peer + v * PS;
+    const bool me = v == R;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) acc[k] += me ? g[k] : row[p0 + k];
+    lacc += me ? loss : row[P];
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) g[k] = acc[k];
+  return lacc;
+}
+
 template <int NPT, int NTHREADS = kBlock>
 DTP_DEV float xgmi_allreduce_model(const DtpTrainArgs& a, int model, int P, float (&g)[NPT], float loss,
                                    unsigned epoch, int tid, unsigned long long* waited = nullptr, int GR = 1,

@@ -98,6 +98,7 @@ class FusedTrainer:
         self._xgmi = None
         self._ring = None
         self.comm_fallback_reason: str | None = None  # why an xGMI setup fell back to RCCL
+        self.groups_refused: str | None = None  # why the split-batch step was not used
         self.comm = self._resolve_comm()
         # DDP construction semantics: every rank starts from rank 0's weights
         if self.world > 1:
@@ -156,6 +157,8 @@ class FusedTrainer:
         if not self.native or self.comm in ("rccl", "host"):
             return 0
         a = self._train_args(1, self._update_mode(), None)
+        if self.groups_refused:
+            a.groups = -1
         return int(nat.load().dtp_mlp_train_lanes(ctypes.byref(a), *self.spec.key[:4], self._update_mode()))
 
     # ------------------------------------------------------------------ setup
@@ -205,6 +208,9 @@ class FusedTrainer:
             self.comm_fallback_reason = why or "a peer failed the xGMI setup or self-test"
             if self.rank == 0:
                 print(f"[dtp] xGMI exchange unavailable ({self.comm_fallback_reason}); using RCCL", flush=True)
+            # the self-test's engine points at the peer buffers about to be unmapped: drop it
+            # (and any graph captured on it) before the switch
+            self._drop_engine()
             if self._xgmi is not None:
                 if dist.is_initialized():
                     comm_util.barrier(self.group)
@@ -367,6 +373,17 @@ class FusedTrainer:
         if self._ring is not None:
             self._ring.ensure(*self._ring.epochs_of_steps(self.t, self.t + k - 1))
 
+    def _drop_engine(self) -> None:
+        """Destroy the native executor and every graph captured on it."""
+        lib = nat.load() if self.native else None
+        if self._engine is not None and lib is not None:
+            lib.dtp_train_engine_destroy(self._engine)
+        self._engine = None
+        for h in list(self._graphs.values()):
+            if isinstance(h, int) and lib is not None:
+                lib.dtp_graph_destroy(ctypes.c_void_p(h))
+        self._graphs.clear()
+
     def _engine_handle(self):
         """The native step executor (created once: argument block, kernel instance and, for
         the split-batch step, its on-chip exchange buffer)."""
@@ -378,6 +395,18 @@ class FusedTrainer:
             e = lib.dtp_train_engine_create(ctypes.byref(a), *self.spec.key[:4], mode)
             if not e:
                 nat.check(-1, "dtp_train_engine_create")
+            gr = lib.dtp_train_engine_groups(e)
+            cus = nat.masked_stream_cus.get(nat.raw_stream(self._dev_index))
+            if gr > 1 and cus is not None and cus < 8 * gr:
+                # the split-batch members spin-wait on each other, so all 8 x groups
+                # workgroups of its grid must be resident at once; a CU-masked stream with
+                # fewer CUs (one workgroup per CU) would never dispatch some of them
+                lib.dtp_train_engine_destroy(e)
+                a.groups = -1
+                e = lib.dtp_train_engine_create(ctypes.byref(a), *self.spec.key[:4], mode)
+                if not e:
+                    nat.check(-1, "dtp_train_engine_create")
+                self.groups_refused = f"{cus} CUs on the masked stream < {8 * gr} split-batch workgroups"
             self._engine = e
             self._engine_run = lib.dtp_train_engine_run
         return e
@@ -602,14 +631,7 @@ class FusedTrainer:
         return self.params[i]
 
     def close(self):
-        lib = nat.load() if self.native else None
-        if self._engine is not None and lib is not None:
-            lib.dtp_train_engine_destroy(self._engine)
-        self._engine = None
-        for k, h in list(self._graphs.items()):
-            if isinstance(h, int) and lib is not None:
-                lib.dtp_graph_destroy(ctypes.c_void_p(h))
-        self._graphs.clear()
+        self._drop_engine()
         if self._xgmi is not None:
             if dist.is_initialized():
                 comm_util.barrier(self.group)

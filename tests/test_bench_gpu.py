@@ -135,3 +135,15 @@ def test_bench_weak_scaling_flag_share_gpu():
     rec = _json_line(r.stdout)
     assert rec["scaling"] == "weak" and rec["config"]["global_batch"] == 512
     assert rec["config"]["per_rank_batch"] == 256 and rec["config"]["dataset_samples"] == 1024
+
+
+def test_bench_cu_mask_keeps_split_batch_resident():
+    """--cu-mask on pins the step to 2 CUs: the split-batch step (8 x 4 co-resident
+    workgroups spinning on each other) cannot run there, so the engine refuses it and
+    runs the one-workgroup-per-model step instead of timing out."""
+    r = subprocess.run([sys.executable, "bench.py", "--cu-mask", "on", "--steps", "50", "--warmup", "5"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = _json_line(r.stdout)
+    assert rec["config"]["cu_mask"] == "on" and rec["config"]["workgroups_per_model"] == 1, rec["config"]
+    assert "groups_refused" in rec["config"]
