@@ -18,11 +18,14 @@ TASKS_PER_NODE=1).  Two engines:
   activation into the next GPU, GPipe micro-batches in wavefront issue order
   (``--microbatches``), per-device DDP buckets reduced from grad-ready hooks
   (``LayerSplitDDP``).
-``--microbatches M`` on the fused engine: the stage kernels hand every sample over its
-own link granules, so each wave's 64 samples cross the stages as an independent
-micro-batch; the math is GPipe's (full-batch gradient, one optimizer step per
-iteration), M only regroups the samples.  Configurations the persistent kernels do not
-cover (batch > 256, other losses) fall back to ``module`` with a printed reason.  Both engines draw the
+``--microbatches M`` on the fused engine: M member workgroups per stage
+(``csrc/split_lanes.hip``), member k of every stage one micro-batch of batch / M <= 64
+samples flowing through the pipeline on its own links (GPipe in space: the M hand-off
+chains run side by side), each stage's member gradients summed on chip before its one
+optimizer step (GPipe's math: the full-batch gradient, one step per iteration).  The
+default (1) picks ceil(batch / 64) members wherever the split-batch stages apply, else
+the one-workgroup stages.  Configurations the persistent kernels do not cover
+(batch > 256, other losses) fall back to ``module`` with a printed reason.  Both engines draw the
 reference's exact DistributedSampler order by default (``--sampler torch``).
 Checkpoint / resume (``--checkpoint_dir --checkpoint_every --resume``) works for
 both.  Launch with torchrun (``--torchrun``) or plain srun exactly like demo.py.
@@ -120,19 +123,14 @@ def main(argv=None):
     if why is None:
         try:
             eng = FusedLayerSplit(toy.spec, devs, ds.X, ds.Y, geom, ocfg, toy.flat_params.detach(), bounds,
-                                  sampler=config.sampler)
-        except NotImplementedError as e:
+                                  sampler=config.sampler,
+                                  members=config.microbatches if config.microbatches > 1 else "auto")
+        except (NotImplementedError, ValueError) as e:  # e.g. more micro-batches than the exchange serves
             why, eng = str(e), None
     if why is None:
-        rank_print(rank, f"engine: fused layer split ({len(devs)} persistent stage kernels)")
-        if config.microbatches > 1:
-            # GPipe semantics are the full-batch gradient and one optimizer step per iteration
-            # (LayerSplitMLP concatenates the micro-batch outputs before the loss); the stage
-            # kernels hand every sample over its own link granules, so each wave's 64 samples
-            # already cross the stages as an independent micro-batch -- M only regroups them
-            rank_print(rank, f"micro-batches: {config.microbatches} requested; the stage kernels stream "
-                             "every wave's 64 samples through the links independently (same gradient, "
-                             "one optimizer step per iteration)")
+        rank_print(rank, f"engine: fused layer split ({len(devs)} persistent stages, "
+                         + (f"{eng.members} member workgroups each: micro-batches of "
+                            f"{-(-geom.batch // eng.members)} samples)" if eng.members else "one workgroup each)"))
         summary = _run_fused(config, eng, geom, world, rank, logger, faults, pbar)
     else:
         if config.engine == "fused":

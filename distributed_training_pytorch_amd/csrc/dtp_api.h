@@ -129,6 +129,9 @@ struct DtpSplitStageArgs {
                           // (device-scope link: plain device memory, sc1); else system scope
   dtp::SamplerCfg smp;
   DtpHyper hp;            // grad_scale = 1 / dp_world
+  // split-batch stages (split_lanes.hip, members > 1 on one rank): the stage's on-chip
+  // member exchange buffer ([2][members][slot16] granules, zeroed), nullable
+  void* grp_buf;
 };
 
 #define DTP_SPLIT_MAX_LOCAL 8
@@ -137,13 +140,17 @@ struct DtpSplitLaunch {
   DtpSplitStageArgs stage[DTP_SPLIT_MAX_LOCAL];
   int shape_id[DTP_SPLIT_MAX_LOCAL];  // dtp_split_shape_id of each stage
   int n;
-  int pad_;
+  int members;  // split_lanes.hip: workgroups per stage (the stage's batch in member slices); else unused
 };
 
 int dtp_split_launch(const DtpSplitLaunch* L, void* stream);
 int dtp_split_shape_id(int in, int h, int nl, int out, int final_act, int first);
 long long dtp_split_link_bytes(int width, int batch);
 int dtp_split_stage_supported(int in, int h, int nl, int out, int final_act, int first);
+// split-batch stages: every stage's batch over L->members workgroups of the 4-lanes schedule
+int dtp_split_lanes_launch(const DtpSplitLaunch* L, void* stream);
+int dtp_split_lanes_supported(int in, int h, int nl, int out, int final_act, int first);
+long long dtp_split_lanes_grp_bytes(int P, int members);
 
 // ---- flat optimizers over [n_models][P] (after an external all-reduce) ----
 struct DtpOptArgs {

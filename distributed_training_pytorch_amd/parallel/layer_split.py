@@ -325,7 +325,7 @@ class FusedLayerSplit:
     def __init__(self, spec: MlpSpec, devices: list[torch.device], X: torch.Tensor, Y: torch.Tensor, geom,
                  optim, init_flat: torch.Tensor, boundaries: list[tuple[int, int]] | None = None, group=None,
                  timeout_us: int = 2_000_000, log_cap: int = 1 << 16, sampler: str = "torch",
-                 launch: str = "per_device"):
+                 launch: str = "per_device", members: int | str = 0):
         import ctypes
 
         from ..ops.optim import OptimConfig
@@ -345,6 +345,7 @@ class FusedLayerSplit:
             raise ValueError("the persistent split step runs one lane per sample: per-rank batch <= 256")
         self.geom = geom
         self.lib = lib = nat.require(self.devices[0])
+        self.members = self._pick_members(members, lib, X, Y, geom)
         for s, ss in enumerate(self.stage_specs):
             if not lib.dtp_split_stage_supported(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
                                                  int(ss.final_act), int(s == 0)):
@@ -391,6 +392,12 @@ class FusedLayerSplit:
             else:
                 self.act_buf[s + 1] = self._alloc(self.devices[s + 1], nbytes)
                 self.grad_buf[s] = self._alloc(self.devices[s], nbytes)
+        # split-batch stages on one rank: each stage's on-chip member exchange buffer
+        self._grp = [None] * K
+        if self.members > 1 and self.world == 1:
+            for s, (ss, dev) in enumerate(zip(self.stage_specs, self.devices)):
+                nb = int(lib.dtp_split_lanes_grp_bytes(ss.P, self.members))
+                self._grp[s] = torch.zeros(nb, dtype=torch.uint8, device=dev)
         # per-stage data-parallel exchange (the stage's gradient over the ranks)
         self._dp = [None] * K
         if self.world > 1:
@@ -473,11 +480,53 @@ class FusedLayerSplit:
                 if dev in self.rings and (s == 0 or s == K - 1):
                     self.rings[dev].native(a.smp)
                 a.hp = self.optim.hyper(spec.slope, 1.0 / self.world)
+                a.grp_buf = nat.ptr(self._grp[s]) if self._grp[s] is not None else None
                 L.shape_id[j] = lib.dtp_split_shape_id(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
                                                        int(ss.final_act), int(s == 0))
+            L.members = self.members
             self._launch[key] = L
+        self._launch_fn = lib.dtp_split_lanes_launch if self.members else lib.dtp_split_launch
         for d in set(self.devices):
             torch.cuda.synchronize(d)
+
+    def _pick_members(self, members, lib, X, Y, geom) -> int:
+        """Workgroups per stage of the split-batch stages (``csrc/split_lanes.hip``): each
+        stage's per-rank batch over M members of <= 64 samples, member k of every stage one
+        micro-batch flowing through the pipeline; 0 = the one-workgroup stages of
+        ``split_train.hip``.  ``auto``: ceil(batch / 64) members wherever every stage has a
+        split-batch instance (the toy model's layer ranges), the sampler reads the device
+        permutation ring and the dataset fits the stages' LDS cache -- else 0.
+        ``DTP_SPLIT_LANES=0`` forces 0 (A/B runs)."""
+        import os
+
+        if members in (0, "off") or os.environ.get("DTP_SPLIT_LANES", "1") == "0":
+            return 0
+        from ..data.sampler import SAMPLER_DIST_SHUFFLE
+
+        K = len(self.stage_specs)
+        ok = all(lib.dtp_split_lanes_supported(ss.in_features, ss.hidden, ss.n_layers, ss.out_features,
+                                               int(ss.final_act), int(s == 0))
+                 for s, ss in enumerate(self.stage_specs))
+        ok = ok and geom.mode == SAMPLER_DIST_SHUFFLE
+        ok = ok and geom.n * X.shape[1] <= 4096 and geom.n * Y.shape[1] <= 4096 and (K > 1 or
+                                                                                  geom.n * (X.shape[1] + Y.shape[1]) <= 4096)
+        need = -(-geom.batch // 64)
+        if members == "auto":
+            m = need
+        else:
+            m = int(members)
+            if m < need:
+                raise ValueError(f"members={m}: a member runs at most 64 samples (batch {geom.batch} needs >= {need})")
+        if m * max(1, self.world) > 8 or m > 8:
+            if members != "auto":
+                raise ValueError(f"members={m} x {self.world} ranks: the exchange serves at most 8")
+            return 0
+        if not ok:
+            if members != "auto":
+                raise ValueError("split-batch stages need the toy layer ranges, the device sampler ring and an "
+                                 "LDS-sized dataset")
+            return 0
+        return m
 
     def _alloc(self, dev: torch.device, nbytes: int) -> int:
         import ctypes
@@ -527,7 +576,7 @@ class FusedLayerSplit:
             for j in range(L.n):
                 L.stage[j].n_steps = n_steps
             with torch.cuda.device(dev):
-                nat.check(self.lib.dtp_split_launch(ctypes.byref(L), nat.stream_ptr(st)), "dtp_split_launch")
+                nat.check(self._launch_fn(ctypes.byref(L), nat.stream_ptr(st)), "dtp_split_launch")
         self._dirty.clear()
         self.t += n_steps
 
@@ -553,6 +602,11 @@ class FusedLayerSplit:
                 raise RuntimeError(f"layer-split link of stage {s} timed out at step {w[1] - 1} (neighbour stalled)")
             if w[2]:
                 raise RuntimeError(f"data-parallel exchange of stage {s} timed out at step {w[3] - 1}")
+        for s, st in enumerate(self.status):
+            w = st[4:6].tolist()
+            if w[0]:
+                raise RuntimeError(f"member exchange of stage {s} timed out at step {w[1] - 1} (a member "
+                                   "workgroup was not resident)")
 
     def losses(self, t0: int, t1: int) -> torch.Tensor:
         self._join()
