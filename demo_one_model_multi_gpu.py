@@ -91,6 +91,15 @@ def _fused_reason(config, devs) -> str | None:
     return None
 
 
+def _members(config, geom):
+    """--microbatches M -> member workgroups per stage of the split-batch stages: M
+    micro-batches of batch / M samples, at least ceil(batch / 64) (a member runs at most
+    64); M = 1: "auto" (ceil(batch / 64) where the split-batch stages apply)."""
+    if config.microbatches <= 1:
+        return "auto"
+    return max(config.microbatches, -(-geom.batch // 64))
+
+
 def _ckpt_due(config, it):
     return bool(config.checkpoint_dir and config.checkpoint_every and it % config.checkpoint_every == 0)
 
@@ -124,7 +133,7 @@ def main(argv=None):
         try:
             eng = FusedLayerSplit(toy.spec, devs, ds.X, ds.Y, geom, ocfg, toy.flat_params.detach(), bounds,
                                   sampler=config.sampler,
-                                  members=config.microbatches if config.microbatches > 1 else "auto")
+                                  members=_members(config, geom))
         except (NotImplementedError, ValueError) as e:  # e.g. more micro-batches than the exchange serves
             why, eng = str(e), None
     if why is None:
@@ -132,6 +141,7 @@ def main(argv=None):
                          + (f"{eng.members} member workgroups each: micro-batches of "
                             f"{-(-geom.batch // eng.members)} samples)" if eng.members else "one workgroup each)"))
         summary = _run_fused(config, eng, geom, world, rank, logger, faults, pbar)
+        summary["members"] = eng.members
     else:
         if config.engine == "fused":
             rank_print(rank, f"engine: module (autograd layer split): {why}")

@@ -30,17 +30,19 @@ from . import comm_util
 
 
 class FlatDDP(nn.Module):
-    # bucket_cap_mb / first_bucket_mb: torch DDP's defaults (25 MB, 1 MiB first bucket,
-    # torch/nn/parallel/distributed.py).  Sizing on one MI355X node: a ring all-reduce
-    # of n bytes over W = 8 ranks moves 2 (W-1)/W n per rank and pays 2 (W-1) hop
-    # latencies; each ring hop is ONE point-to-point xGMI link, so RCCL runs several
-    # rings side by side over the 7 links.  Per bucket the fixed cost is the RCCL launch
-    # plus 14 hops (~10-20 us); at tens of GB/s per ring a 25 MB bucket spends > 90 % of
-    # its time moving bytes, while the 1 MiB first bucket starts the exchange as soon as
-    # the last layer's gradients exist.  Buckets <= 64 Ki floats take the one-shot xGMI
-    # all-reduce instead (one posted write per peer, one hop).  The 64 MB cap of round 3
-    # had no measurement behind it; no multi-GPU node was available to A/B either value.
-    def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
+    # bucket_cap_mb / first_bucket_mb: "auto" (default) measures the all-reduce of this
+    # process group on this node at construction (parallel/bucket_tuning.py: latency
+    # alpha and bandwidth beta fitted to a few probe sizes; cap = 9 alpha beta, first =
+    # alpha beta) when there are several ranks and a gradient bigger than the smallest
+    # probe; otherwise -- and for any explicit number -- torch DDP's defaults (25 MB,
+    # 1 MiB first bucket, torch/nn/parallel/distributed.py).  Why measure: on one MI355X
+    # node a ring all-reduce of n bytes over W ranks moves 2 (W-1)/W n per rank and pays
+    # 2 (W-1) hop latencies, each hop ONE point-to-point xGMI link; the crossover between
+    # latency and bytes is a property of the node and RCCL version, not a constant.
+    # Buckets <= 64 Ki floats take the one-shot xGMI all-reduce instead (one posted write
+    # per peer, one hop).  ``bucket_plan`` records what was chosen and from what.
+    def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float | str = "auto",
+                 first_bucket_mb: float | str = "auto",
                  flat_params: torch.Tensor | None = None, flat_grad: torch.Tensor | None = None,
                  broadcast: bool = True, comm: str = "auto"):
         super().__init__()
@@ -64,6 +66,7 @@ class FlatDDP(nn.Module):
                     p.grad.data_ptr() + p.numel() * p.element_size() > base + flat_grad.numel() * flat_grad.element_size():
                 raise ValueError("parameter grads must be views of flat_grad")
             self._offset[p] = (p.grad.data_ptr() - base) // p.element_size()
+        bucket_cap_mb, first_bucket_mb = self._resolve_buckets(params, bucket_cap_mb, first_bucket_mb)
         # buckets in reverse registration order (~ the order backward produces grads)
         self._buckets = []
         cur, cur_bytes = [], 0
@@ -142,6 +145,26 @@ class FlatDDP(nn.Module):
             why = why or "self-test failed on another rank"
         if strict and self.world > 1:
             raise RuntimeError(f"FlatDDP comm='xgmi' unavailable: {why}")
+
+    def _resolve_buckets(self, params, cap_mb, first_mb) -> tuple[float, float]:
+        """Numbers as given; "auto": the measured plan (bucket_tuning.plan) with several
+        ranks and a gradient larger than the smallest probe, else torch's defaults."""
+        from . import bucket_tuning
+
+        self.bucket_plan = {"source": "default", "first_bucket_mb": 1.0, "bucket_cap_mb": 25.0}
+        if "auto" in (cap_mb, first_mb):
+            total = sum(p.numel() * p.element_size() for p in params)
+            if self.world > 1 and total > min(bucket_tuning.DEFAULT_SIZES):
+                dev = self.flat_grad.device
+                backend = dist.get_backend(self.group)
+                self.bucket_plan = dict(bucket_tuning.plan(self.group,
+                                                           dev if backend == "nccl" else torch.device("cpu")))
+        else:
+            self.bucket_plan = {"source": "explicit"}
+        cap = self.bucket_plan["bucket_cap_mb"] if cap_mb == "auto" else float(cap_mb)
+        first = self.bucket_plan["first_bucket_mb"] if first_mb == "auto" else float(first_mb)
+        self.bucket_plan.update(bucket_cap_mb=cap, first_bucket_mb=first)
+        return cap, first
 
     @staticmethod
     def _flatten(params):

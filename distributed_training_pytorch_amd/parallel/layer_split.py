@@ -325,7 +325,7 @@ class FusedLayerSplit:
     def __init__(self, spec: MlpSpec, devices: list[torch.device], X: torch.Tensor, Y: torch.Tensor, geom,
                  optim, init_flat: torch.Tensor, boundaries: list[tuple[int, int]] | None = None, group=None,
                  timeout_us: int = 2_000_000, log_cap: int = 1 << 16, sampler: str = "torch",
-                 launch: str = "per_device", members: int | str = 0):
+                 launch: str = "per_device", members: int | str = "auto"):
         import ctypes
 
         from ..ops.optim import OptimConfig

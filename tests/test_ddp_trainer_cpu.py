@@ -127,6 +127,52 @@ def test_flatddp_in_place_gemm_grads_match_torch_ddp():
     assert torch.equal(res[0][0], res[1][0])
 
 
+def _flatddp_auto_buckets(rank, world):
+    from distributed_training_pytorch_amd.models.wide import WideMLP
+    from distributed_training_pytorch_amd.parallel import bucket_tuning
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    # small probes on the CPU ranks (the node's defaults go to 64 MB)
+    bucket_tuning.DEFAULT_SIZES = (16 << 10, 64 << 10, 256 << 10, 1 << 20)
+    torch.manual_seed(0)
+    m = WideMLP((2, 256, 256, 256, 1))  # ~133 K parameters: larger than the smallest probe
+    ddp = FlatDDP(m)
+    plan = ddp.bucket_plan
+    toy = FlatDDP(ModelBank(2))  # 3 KB of gradients: nothing to choose, no measurement
+    g = torch.Generator().manual_seed(rank)
+    x, y = torch.randn(16, 2, generator=g), torch.randn(16, 1, generator=g)
+    ddp.zero_grad()
+    torch.nn.functional.mse_loss(ddp(x), y).backward()
+    return plan, toy.bucket_plan, len(ddp._buckets), ddp.flat_grad.clone()
+
+
+def test_flatddp_auto_buckets_measured_on_the_group():
+    """bucket_cap_mb / first_bucket_mb = "auto": every rank measures the group's all-reduce
+    at a few sizes, fits t = alpha + n / beta and takes the same plan (the slowest rank's
+    medians); a model that fits the smallest probe keeps torch's defaults unmeasured."""
+    res = run_ranks(_flatddp_auto_buckets, 2)
+    plan0, toy0, nb0, g0 = res[0]
+    plan1, _, nb1, g1 = res[1]
+    assert plan0["source"] == "measured" and plan0 == plan1 and nb0 == nb1
+    assert plan0["alpha_us"] >= 0 and plan0["bandwidth_GBps"] > 0 and len(plan0["measured"]) == 4
+    assert 1.0 <= plan0["bucket_cap_mb"] <= 256.0
+    assert 64 / 1024 <= plan0["first_bucket_mb"] <= plan0["bucket_cap_mb"]
+    assert toy0["source"] == "default" and toy0["bucket_cap_mb"] == 25.0
+    assert torch.equal(g0, g1)  # the averaged gradient is the same on both ranks
+
+
+def test_bucket_choice_from_a_latency_bandwidth_fit():
+    from distributed_training_pytorch_amd.parallel import bucket_tuning
+
+    alpha, beta = 20e-6, 50e9  # 20 us fixed, 50 GB/s
+    meas = [(n, alpha + n / beta) for n in (1 << 20, 4 << 20, 16 << 20, 64 << 20)]
+    a, b = bucket_tuning.fit_latency_bandwidth(meas)
+    assert abs(a - alpha) < 1e-9 and abs(b - beta) / beta < 1e-6
+    p = bucket_tuning.choose_buckets(meas)
+    assert abs(p["bucket_cap_mb"] - 9 * alpha * beta / 2 ** 20) < 1e-3  # 8.6 MB: 10 % fixed cost
+    assert abs(p["first_bucket_mb"] - alpha * beta / 2 ** 20) < 1e-3  # 0.95 MB: half bytes, half latency
+
+
 def _lit_run(tmp_path, steps, ckpt_path=None, every=0, precision=32):
     sys.path.insert(0, str(ROOT))
     from demo_pytorch_lightning import LitToyModel
