@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--groups", choices=["auto", "on", "off"], default="auto",
                     help="split-batch step (csrc/grp_core.h): a rank's batch over batch/64 workgroups per model; "
                          "auto = the measured policy")
+    ap.add_argument("--stream", choices=["default", "pool"], default="default",
+                    help="default: the device's default (null) stream; pool: a torch pool stream (non-blocking), "
+                         "so the step's launches never synchronise with other blocking streams")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:(local_rank %% device_count), gloo process group "
@@ -244,6 +247,8 @@ def main():
             from distributed_training_pytorch_amd import _native
 
             torch.cuda.set_stream(_native.cu_masked_stream(dev, [0, 1]))
+        elif a.stream == "pool" and dev.type == "cuda":
+            torch.cuda.set_stream(torch.cuda.Stream(device=dev))
         X, Y = ds.device_tensors(dev)
         geom = SamplerGeometry(n=n, world=world, rank=rank, batch=a.batch, seed=a.seed)
         torch.manual_seed(a.seed)
@@ -262,7 +267,7 @@ def main():
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm,
                     "host_cpu": pinned,
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
-                    else "Feistel shuffle", "cu_mask": a.cu_mask,
+                    else "Feistel shuffle", "cu_mask": a.cu_mask, "stream": a.stream,
                     # lanes per sample of the fused step (1, or 2 / 4: csrc/mlp_lanes.h for batches <= 128 / 64)
                     "lanes_per_sample": runner.lanes, "waves_per_cu": runner.kernel_waves,
                     # > 1: the split-batch step (csrc/grp_core.h), CUs per model

@@ -170,7 +170,7 @@ class OptArgs(ctypes.Structure):
         ("P", c_int),
         ("kind", c_int),
         ("loss_scale", c_float),
-        ("pad_", c_int),
+        ("flags", c_int),
         ("hp", Hyper),
         ("shadow", c_void_p),
         ("shadow_ld", c_longlong),
@@ -235,6 +235,7 @@ def _declare(lib):
         "dtp_mlp_train_profile": (c_int, [P(TrainArgs), c_void_p]),
         "dtp_xgmi_fused_buffer_bytes": (c_longlong, [c_int, c_int, c_int]),
         "dtp_train_engine_create": (c_void_p, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
+        "dtp_train_engine_poison": (c_int, [c_void_p, c_int]),
         "dtp_train_engine_run": (c_int, [c_void_p, c_int, c_int, c_void_p]),
         "dtp_train_engine_destroy": (None, [c_void_p]),
         "dtp_train_engine_lanes": (c_int, [c_void_p]),

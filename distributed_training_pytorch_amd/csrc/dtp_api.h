@@ -165,12 +165,13 @@ struct DtpOptArgs {
   int P;
   int kind;           // DTP_MODE_ADAM or DTP_MODE_SGD
   float loss_scale;   // applied to the all-reduced losses (1/world)
-  int pad_;
+  int flags;          // DTP_OPT_ZERO_GRAD: write 0 over every gradient element once read
   DtpHyper hp;
   void* shadow;       // [n_models][shadow_ld] bf16 copy of the updated params, or null
   long long shadow_ld;  // row stride of shadow in elements (>= P)
 };
 
+#define DTP_OPT_ZERO_GRAD 1
 int dtp_flat_optimizer(const DtpOptArgs* a, void* stream);
 
 // ---- MFMA GEMM with fused Linear epilogues (gemm.hip) ----

@@ -54,6 +54,37 @@ DTP_HD double pow_int(double b, uint64_t e) {
   return r;
 }
 
+// dst[0 .. na) = A[0 .. na), dst[na .. na + nb) = B[0 .. nb) (global -> LDS) in two halves:
+// load() issues every global load of this thread into registers, store() writes them to
+// LDS.  A plain `for (e = tid; e < n; e += NTH) dst[e] = src[e]` loop with a runtime trip
+// count waits out its loads chunk by chunk before the stores -- several memory round trips
+// per launch prologue (scripts/k20_prologue.py: 7.4 k cycles from kernel entry to the
+// first barrier); issued with the prologue's other loads, the fill costs none of its own.
+// Requires na + nb <= MAXE (checked by the host).
+template <int MAXE, int NTH>
+struct LdsFill2 {
+  static constexpr int J = (MAXE + NTH - 1) / NTH;
+  float v[J];
+  int n;
+  DTP_DEV void load(const float* __restrict__ A, int na, const float* __restrict__ B, int nb, int tid) {
+    n = na + nb;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int e = tid + j * NTH;
+      v[j] = 0.f;
+      if (e < na) v[j] = A[e];
+      else if (e - na < nb) v[j] = B[e - na];
+    }
+  }
+  DTP_DEV void store(float* __restrict__ dst, int tid) const {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int e = tid + j * NTH;
+      if (e < n) dst[e] = v[j];
+    }
+  }
+};
+
 // error reporting shared by every translation unit (defined in runtime.hip)
 int set_err(int code, const char* msg);
 int check_launch(const char* what);

@@ -85,10 +85,11 @@ int dtp_gather_rows2(const float* X, int dx, const float* Y, int dy, const long 
 }
 
 // the single-workgroup forward serves up to kMseMax elements (beyond: the caller's torch path)
-long long dtp_mse_max_elems() { return 1ll << 20; }
+// (64 Ki: one CU streams 512 KiB in a few us; beyond that torch's multi-block reduction is faster)
+long long dtp_mse_max_elems() { return 1ll << 16; }
 
 int dtp_mse_fwd(const float* a, const float* b, long long n, float* out, void* stream) {
-  if (!a || !b || !out || n <= 0 || n > dtp_mse_max_elems()) return dtp::set_err(-1, "mse_fwd: 1..2^20 elements");
+  if (!a || !b || !out || n <= 0 || n > dtp_mse_max_elems()) return dtp::set_err(-1, "mse_fwd: 1..2^16 elements");
   hipLaunchKernelGGL(dtp::mse_fwd_kernel, dim3(1), dim3(dtp::kBlock), 0, (hipStream_t)stream, a, b, n,
                      1.f / (float)n, out);
   return dtp::check_launch("mse_fwd_kernel");

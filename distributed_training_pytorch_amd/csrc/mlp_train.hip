@@ -674,6 +674,10 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     mr[k] = own ? a.opt_m[(size_t)model * P + p] : 0.f;
     vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
   }
+  // the dataset (inputs then targets) into registers with the other prologue loads; into
+  // LDS after the first wait
+  LdsFill2<kLaneData, NTH> dfill;
+  dfill.load(a.X, smp.n * S::IN, a.Y, smp.n * YD, tid);
   // split-batch publisher (wave 0, DTP_GRP_DIRECT): the dW-tile positions of the parameters of
   // its granules q = tid + 64 j (granule q holds parameters NPT (q / GPT) + 2 (q % GPT), + 1;
   // the last granule is the loss), so it sums them straight from the tiles
@@ -735,8 +739,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   bool gplain = false;
   unsigned long long xwait[2] = {0ull, 0ull};
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
-  for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
-  for (int e = tid; e < smp.n * YD; e += NTH) sm.data[smp.n * S::IN + e] = a.Y[e];
+  dfill.store(sm.data, tid);
   const int yoff = smp.n * S::IN;
   stamp_launch(18);
   // this wave's staging areas: zero (unwritten rows / columns stay finite), then the
@@ -857,10 +860,11 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       const int cls = valid ? (int)ny[0] : 0;
       float mx = out[0];
       static_for<1, S::OUT>([&](auto JC) { mx = fmaxf(mx, out[decltype(JC)::value]); });
-      float se = 0.f, zc = 0.f;
+      float se = 0.f, zc = 0.f, ex[S::OUT];  // each exponential once (the same bits as twice)
       static_for<0, S::OUT>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        se += __expf(out[j] - mx);
+        ex[j] = __expf(out[j] - mx);
+        se += ex[j];
         zc = (j == cls) ? out[j] : zc;
       });
       const float lse = mx + __logf(se);
@@ -868,7 +872,7 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
       lpart = valid ? lse - zc : 0.f;
       static_for<0, S::OUT>([&](auto JC) {
         constexpr int j = decltype(JC)::value;
-        dzl[j] = valid ? S::rnd((__expf(out[j] - mx) * rs - (j == cls ? 1.f : 0.f)) * inv) : 0.f;
+        dzl[j] = valid ? S::rnd((ex[j] * rs - (j == cls ? 1.f : 0.f)) * inv) : 0.f;
       });
     }
     DTP_STAMP(2);
@@ -1145,6 +1149,12 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   }
 
   stamp_launch(24);
+  if constexpr (GRP || kXgmi) {
+    // a launch whose exchange timed out on any thread keeps the state from before it (what
+    // it summed is incomplete; check_comm raises on the status word), so a checkpoint or a
+    // resume never sees it -- one barrier per launch
+    if (__syncthreads_or(xdead ? 1 : 0)) return;
+  }
   if (!lead) return;  // every member holds the same state: the first writes it back
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -1418,6 +1428,18 @@ TrainLaunchFn resolve_train(const DtpTrainArgs& a, int in, int h, int nl, int ou
   LanePick lp = pick_lanes(a, in, out, base);
   if (base) {
     const int gr = pick_groups(a, in, out, allow_groups, fast);
+    // A/B only (DTP_GRP_NW=8): the split-batch step on members of 128 samples, each the
+    // two-waves-per-SIMD 4-lanes step (8 waves), half the members of the default -- toy
+    // fp32 Adam + MSE at one rank (docs/perf_notes.md "Round 6: two members")
+    static const bool nw8 = getenv("DTP_GRP_NW") && atoi(getenv("DTP_GRP_NW")) == 8;
+    if (nw8 && gr > 1 && mode == DTP_MODE_ADAM && !ce && !a.bf16 && in == 2 && h == 10 && nl == 5 && out == 1) {
+      const int b = min(a.smp.batch, a.smp.num_samples);
+      const int gr8 = (b + 127) / 128;
+      if (gr8 > 1 && a.smp.n * (in + out) <= dtp::kLaneData) {
+        if (pick) *pick = LanePick{4, 8, gr8};
+        return &launch_lanes_grp<dtp::Stage<2, 10, 5, 1, false>, 4, 8>;
+      }
+    }
     if (gr > 1) {
       if (TrainLaunchFn f = grp_inst(in, h, nl, out, mode, ce, a.bf16)) {
         if (pick) *pick = LanePick{4, 4, gr};
@@ -1641,6 +1663,17 @@ int dtp_train_engine_status(void* h, int* out2) {
   if (!e->a.grp_status) return 0;
   if (hipMemcpy(out2, e->a.grp_status, 2 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
     return set_err(-3, "status copy failed");
+  return 0;
+}
+
+// test hook: mark the split-batch exchange as timed out at `epoch` (sticky, as a real
+// timeout would), so the next launch runs dead -- and must leave the state untouched
+int dtp_train_engine_poison(void* h, int epoch) {
+  auto* e = static_cast<TrainEngine*>(h);
+  if (!e || !e->a.grp_status) return set_err(-1, "no split-batch exchange");
+  const int w[2] = {1, epoch};
+  if (hipMemcpy(e->a.grp_status, w, sizeof w, hipMemcpyHostToDevice) != hipSuccess)
+    return set_err(-3, "status write failed");
   return 0;
 }
 

@@ -23,6 +23,10 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
   float* m = a.opt_m + (size_t)model * a.P;
   float* v = a.opt_v ? a.opt_v + (size_t)model * a.P : nullptr;
   const float* g = a.grad + (size_t)model * a.P;
+  // DTP_OPT_ZERO_GRAD: the consumed gradient is zeroed in the same pass (the Trainer's
+  // module path then needs no zero_grad fill launch before the next backward)
+  const bool zg = a.flags & DTP_OPT_ZERO_GRAD;
+  float* const gz = const_cast<float*>(g);
   __bf16* sh = a.shadow ? reinterpret_cast<__bf16*>(a.shadow) + (size_t)model * a.shadow_ld : nullptr;
   // float4 body: the four rows share their offset within 16 bytes (same [n][P] layout
   // on 16-byte aligned bases), so `head` scalar elements (0-3) bring every row to a
@@ -44,6 +48,7 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < P4; i += gridDim.x * kBlock) {
       float4 w = p4[i], mi = m4[i], vi = v4[i];
       const float4 gi = g4[i];
+      if (zg) reinterpret_cast<float4*>(gz + head)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       adam_update(w.x, mi.x, vi.x, gi.x * a.hp.grad_scale, s);
       adam_update(w.y, mi.y, vi.y, gi.y * a.hp.grad_scale, s);
       adam_update(w.z, mi.z, vi.z, gi.z * a.hp.grad_scale, s);
@@ -58,7 +63,9 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
     const int idx = e < head ? e : (e - head < a.P - tail0 ? tail0 + e - head : -1);
     if (idx >= 0) {
       float w = p[idx], mi = m[idx], vi = v[idx];
-      adam_update(w, mi, vi, g[idx] * a.hp.grad_scale, s);
+      const float gv = g[idx];
+      if (zg) gz[idx] = 0.f;
+      adam_update(w, mi, vi, gv * a.hp.grad_scale, s);
       p[idx] = w;
       m[idx] = mi;
       v[idx] = vi;
@@ -78,6 +85,10 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
       const float g0 = g[i];
       float w1 = 0.f, m1 = 0.f, v1 = 0.f, g1 = 0.f;
       if (two) w1 = p[i + 1], m1 = m[i + 1], v1 = v[i + 1], g1 = g[i + 1];
+      if (zg) {
+        gz[i] = 0.f;
+        if (two) gz[i + 1] = 0.f;
+      }
       adam_update(w0, m0, v0, g0 * a.hp.grad_scale, s);
       p[i] = w0;
       m[i] = m0;
@@ -96,7 +107,9 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
     const AdamScalars s = adam_scalars(a.hp, t + 1);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.P; i += gridDim.x * kBlock) {
       float w = p[i], mi = m[i], vi = v[i];
-      adam_update(w, mi, vi, g[i] * a.hp.grad_scale, s);
+      const float gv = g[i];
+      if (zg) gz[i] = 0.f;
+      adam_update(w, mi, vi, gv * a.hp.grad_scale, s);
       p[i] = w;
       m[i] = mi;
       v[i] = vi;
@@ -105,7 +118,9 @@ __global__ __launch_bounds__(kBlock) void flat_optimizer_kernel(DtpOptArgs a) {
     const float lr = (float)a.hp.lr, mom = (float)a.hp.momentum, wd = (float)a.hp.weight_decay;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.P; i += gridDim.x * kBlock) {
       float w = p[i], bi = m[i];
-      sgd_update(w, bi, g[i] * a.hp.grad_scale, lr, mom, wd, t == 0);
+      const float gv = g[i];
+      if (zg) gz[i] = 0.f;
+      sgd_update(w, bi, gv * a.hp.grad_scale, lr, mom, wd, t == 0);
       p[i] = w;
       m[i] = bi;
       if (sh) sh[i] = (__bf16)w;

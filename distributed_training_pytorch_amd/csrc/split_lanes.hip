@@ -212,13 +212,13 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
     sl_pos<S, FIRST, LAST>(own ? p : 0, pf[k], pb[k], tp[k]);
     if (!own) pf[k] = pb[k] = C::pad4(C::LW);  // the sink
   }
+  // inputs (first stage) then targets (last stage): issued with the loads above
+  LdsFill2<kSLData, NTH> dfill;
+  dfill.load(a.X, FIRST ? smp.n * S::IN : 0, a.Y, LAST ? smp.n * S::OUT : 0, tid);
   const int t0 = a.step[0];
   for (int e = tid; e < C::pad4(C::LW) + 4; e += NTH) sm.wb[e] = 0.f;
-  if constexpr (FIRST)
-    for (int e = tid; e < smp.n * S::IN; e += NTH) sm.data[e] = a.X[e];
   constexpr int XW = FIRST ? S::IN : 0;
-  if constexpr (LAST)
-    for (int e = tid; e < smp.n * S::OUT; e += NTH) sm.data[smp.n * XW + e] = a.Y[e];
+  dfill.store(sm.data, tid);
   {  // this wave's staging areas: zero, then the constant-1 bias column of every layer
     float* s0 = &sm.stg[wave][0][0];
     for (int e = lane; e < NL * 2 * C::AREA; e += kWave) s0[e] = 0.f;
@@ -578,6 +578,8 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
       __syncthreads();
     }
   }
+  // a launch whose link or gradient exchange timed out keeps the state from before it
+  if (__syncthreads_or((link_dead || xdead) ? 1 : 0)) return;
   if (!lead) return;  // every member holds the same state: the first writes it back
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {

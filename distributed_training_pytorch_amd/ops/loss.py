@@ -22,7 +22,7 @@ from .. import _native as nat
 
 def _fused_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     return (a.is_cuda and b.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
-            and a.shape == b.shape and a.device == b.device and 0 < a.numel() <= (1 << 20)
+            and a.shape == b.shape and a.device == b.device and 0 < a.numel() <= (1 << 16)
             and nat.native_enabled())
 
 

@@ -109,13 +109,15 @@ def sgd_update_ref(p: torch.Tensor, buf: torch.Tensor, g: torch.Tensor, first: b
 
 
 def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: float = 1.0,
-                        loss_log=None, loss_scale: float = 1.0, slope: float = 0.01, shadow=None) -> None:
+                        loss_log=None, loss_scale: float = 1.0, slope: float = 0.01, shadow=None,
+                        zero_grad: bool = False) -> None:
     """One optimizer step over [n_models, P] flat buffers.
 
     ``grad`` is [n_models*P (+ n_models losses)] -- the all-reduced comm buffer;
     ``step`` is the per-model int32 step counter (device or CPU); ``shadow`` (optional,
     bf16 [n_models, >= P], unit column stride) receives the updated parameters rounded
-    to bf16 in the same pass, row i at ``shadow[i, :P]``.
+    to bf16 in the same pass, row i at ``shadow[i, :P]``.  ``zero_grad``: the gradient
+    rows are zeroed in the same pass once read (the loss slots are not).
     """
     n_models, P = params.shape
     if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.dim() != 2 or shadow.shape[0] != n_models
@@ -125,7 +127,7 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
         lib = nat.require(params.device)
         a = nat.OptArgs(nat.ptr(params), nat.ptr(m), nat.ptr(v), nat.ptr(step), nat.ptr(grad),
                         nat.ptr(loss_log), 0 if loss_log is None else loss_log.shape[0], n_models, P, cfg.kind,
-                        loss_scale, 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow),
+                        loss_scale, 1 if zero_grad else 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow),
                         0 if shadow is None else shadow.stride(0))
         nat.check(lib.dtp_flat_optimizer(ctypes.byref(a), nat.stream_ptr()), "dtp_flat_optimizer")
         return
@@ -139,6 +141,8 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
         if loss_log is not None:
             loss_log[t % loss_log.shape[0], i] = grad[n_models * P + i] * loss_scale
         step[i] = t + 1
+    if zero_grad:
+        grad[: n_models * P].zero_()
     if shadow is not None:
         shadow[:, :P].copy_(params)
 
@@ -166,7 +170,10 @@ class FlatOptimizer:
         self.slope = slope
 
     @torch.no_grad()
-    def step(self) -> None:
+    def step(self, zero_grad: bool = False) -> bool:
+        """One step; ``zero_grad``: zero the gradient in the same launch (no separate fill
+        before the next backward).  Returns whether the gradient was zeroed (not when it
+        had to be staged through a copy)."""
         # the kernel reads grad[i*P : (i+1)*P] only (the loss slots behind them are
         # read only with a loss log), so a contiguous [n, P] gradient is used in place
         n, P = self.params.shape
@@ -175,12 +182,14 @@ class FlatOptimizer:
         else:
             self._buf[: n * P].copy_(self.grad.reshape(-1))
             buf = self._buf
+            zero_grad = False
         sh = self.shadow
         fresh = sh is not None and sh._token == sh._current()  # else the next forward re-casts anyway
         flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.cfg, slope=self.slope,
-                            shadow=sh.buf if fresh else None)
+                            shadow=sh.buf if fresh else None, zero_grad=zero_grad)
         if fresh:
             sh.mark_fresh()
+        return zero_grad
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         self.grad.zero_()

@@ -241,7 +241,17 @@ class FlatDDP(nn.Module):
         self._callback_queued = False
 
     def zero_grad(self):
+        """Zero the flat gradient -- unless the last optimizer step already did
+        (``mark_grad_clean``: the flat optimizer zeroes what it consumed), which saves a
+        fill launch per optimizer step."""
+        if getattr(self, "_grad_clean", False):
+            self._grad_clean = False
+            return
         self.flat_grad.zero_()
+
+    def mark_grad_clean(self):
+        """The whole flat gradient is zero now (set by the caller that zeroed it)."""
+        self._grad_clean = True
 
     def reset_hooks(self):
         """Forget a backward that never finished (e.g. an aborted graph capture)."""

@@ -217,6 +217,7 @@ class Trainer:
         # run a plain torch Adam/SGD over a flat-buffer span as ONE flat-optimizer kernel (GPU)
         self.native_optimizers = native_optimizers
         self._flat_opts: list = []
+        self._opt_zeroes = False  # the flat optimizers zero the gradient they consume (fit)
         self.graph_replays = 0
         self.global_step = 0
         self.current_epoch = 0
@@ -301,6 +302,13 @@ class Trainer:
         ddp = FlatDDP(model) if (self.world_size > 1 or single_ok) else None
         loader = self._loader(dl)
         self._flat_opts = [_flat_optimizer_for(o, ddp) if self.native_optimizers else None for o in opts]
+        # every trainable parameter under exactly one flat optimizer (one optimizer, or
+        # several toggled per PL 1.5 so a backward touches only the stepping optimizer's
+        # gradients): each flat step leaves the whole flat gradient zero
+        self._opt_zeroes = False
+        if ddp is not None and self._flat_opts and all(f is not None for f in self._flat_opts):
+            owned = [id(p) for f in self._flat_opts for p in f.params]
+            self._opt_zeroes = len(owned) == len(set(owned)) and set(owned) == {id(p) for p in ddp._params}
         stepper, static = self._batch_stepper(model, ddp, opts)
         logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
@@ -728,6 +736,7 @@ class Trainer:
             if r is None:
                 fo.export_state()
                 self._flat_opts[i] = None
+                self._opt_zeroes = False  # torch's step leaves its gradient: zero_grad fills again
                 changed = True
             else:
                 changed |= r
@@ -756,7 +765,9 @@ class Trainer:
             loss.backward(self._backward_seed(loss))
             flat = self._flat_opts[oi] if oi < len(self._flat_opts) else None
             if flat is not None:
-                flat.step()
+                # the flat kernel zeroes the gradient it consumed: the next zero_grad is free
+                if flat.step(zero_grad=self._opt_zeroes) and ddp is not None:
+                    ddp.mark_grad_clean()
             else:
                 opt.step()
             if len(opts) > 1:
@@ -943,8 +954,8 @@ class _FlatTorchOptimizer:
         self.cfg = self.flat.cfg = cfg
         return True
 
-    def step(self):
-        self.flat.step()
+    def step(self, zero_grad: bool = False) -> bool:
+        return self.flat.step(zero_grad=zero_grad)
 
     def export_state(self):
         step = int(self.flat.step_ctr[0].item())

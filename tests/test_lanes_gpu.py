@@ -227,3 +227,28 @@ def test_two_waves_per_simd_instances_match_torch(force, batch, tmp_path):
     ref_p, ref_l = torch_train(TOY_SPEC, res["init"], X, Y, [EpochIndexStream(geom)], steps, OptimConfig(lr=1e-2))
     torch.testing.assert_close(res["l"], ref_l, rtol=2e-4, atol=1e-5)
     torch.testing.assert_close(res["p"], ref_p, rtol=1e-4, atol=2e-5)
+
+
+def test_split_batch_dead_launch_keeps_the_state():
+    """A launch whose member exchange timed out (sticky status word) sums incomplete
+    gradients: it must write nothing back -- parameters, moments and step counters stay
+    those before it -- and check_comm must raise."""
+    import ctypes
+
+    from distributed_training_pytorch_amd import _native as nat
+
+    X, Y = ToyData(n=512, seed=21).device_tensors(DEV)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, SamplerGeometry(n=512, batch=256, seed=3), OptimConfig(lr=1e-2),
+                      EngineConfig(groups="on"), init_params=_init(TOY_SPEC, 4))
+    assert tr.groups == 4
+    tr.train(5)
+    tr.synchronize()
+    before = [t.clone() for t in (tr.params, tr.m, tr.v, tr.step_ctr)]
+    nat.check(nat.load().dtp_train_engine_poison(ctypes.c_void_p(tr._engine), 6), "poison")
+    tr.train(3)
+    torch.cuda.synchronize()
+    for a, b in zip(before, (tr.params, tr.m, tr.v, tr.step_ctr)):
+        assert torch.equal(a, b)
+    with pytest.raises(RuntimeError, match="timed out"):
+        tr.check_comm()
+    tr.close()

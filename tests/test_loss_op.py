@@ -15,7 +15,7 @@ def test_mse_loss_cpu_falls_back_to_torch():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(128, 1), (256, 4), (1000,), (70000, 3)])
+@pytest.mark.parametrize("shape", [(128, 1), (256, 4), (1000,), (21000, 3)])
 def test_mse_loss_fused_matches_torch(shape):
     from distributed_training_pytorch_amd import _native as nat
 
@@ -33,6 +33,17 @@ def test_mse_loss_fused_matches_torch(shape):
     (3.0 * ref).backward()
     torch.testing.assert_close(a.grad, a2.grad, rtol=1e-5, atol=1e-8)
     torch.testing.assert_close(b.grad, b2.grad, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_mse_loss_large_inputs_take_torchs_reduction():
+    """Above 64 Ki elements the one-workgroup forward would stream everything through one
+    CU: torch's multi-block reduction runs instead (same values)."""
+    a = torch.randn(70000, 3, device="cuda", requires_grad=True)
+    b = torch.randn(70000, 3, device="cuda")
+    out = mse_loss(a, b)
+    assert "FusedMSE" not in type(out.grad_fn).__name__
+    torch.testing.assert_close(out, torch.nn.functional.mse_loss(a, b))
 
 
 @pytest.mark.gpu
