@@ -250,6 +250,8 @@ def _declare(lib):
         "dtp_mse_max_elems": (c_longlong, []),
         "dtp_mse_fwd": (c_int, [c_void_p, c_void_p, c_longlong, c_void_p, c_void_p]),
         "dtp_mse_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_void_p, c_void_p, c_void_p]),
+        "dtp_mse_pair_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_void_p, c_void_p, c_void_p, c_void_p]),
+        "dtp_mse_pair_bwd": (c_int, [c_void_p] * 6 + [c_longlong] + [c_void_p] * 4),
         "dtp_gather_rows2": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_longlong, c_void_p, c_void_p,
                                      c_void_p]),
         "dtp_randperm_fill": (c_int, [ctypes.c_ulonglong, c_int, c_longlong, c_int, c_void_p, c_int]),

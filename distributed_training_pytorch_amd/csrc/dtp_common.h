@@ -54,36 +54,31 @@ DTP_HD double pow_int(double b, uint64_t e) {
   return r;
 }
 
-// dst[0 .. na) = A[0 .. na), dst[na .. na + nb) = B[0 .. nb) (global -> LDS) in two halves:
-// load() issues every global load of this thread into registers, store() writes them to
-// LDS.  A plain `for (e = tid; e < n; e += NTH) dst[e] = src[e]` loop with a runtime trip
-// count waits out its loads chunk by chunk before the stores -- several memory round trips
-// per launch prologue (scripts/k20_prologue.py: 7.4 k cycles from kernel entry to the
-// first barrier); issued with the prologue's other loads, the fill costs none of its own.
-// Requires na + nb <= MAXE (checked by the host).
-template <int MAXE, int NTH>
-struct LdsFill2 {
-  static constexpr int J = (MAXE + NTH - 1) / NTH;
-  float v[J];
-  int n;
-  DTP_DEV void load(const float* __restrict__ A, int na, const float* __restrict__ B, int nb, int tid) {
-    n = na + nb;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int e = tid + j * NTH;
-      v[j] = 0.f;
-      if (e < na) v[j] = A[e];
-      else if (e - na < nb) v[j] = B[e - na];
-    }
+typedef __attribute__((address_space(3))) void dtp_lds_void_t;
+typedef __attribute__((address_space(1))) void dtp_gbl_void_t;
+
+// dst[0 .. na) = A[0 .. na), dst[na .. na + nb) = B[0 .. nb) (global -> LDS) by LDS-DMA
+// (global_load_lds_dword: no staging registers, no wait inside the loop -- every wave
+// issues its ceil((na + nb) / NTH) copies back to back; the caller's next __syncthreads
+// waits them out).  The launch prologue is instruction-fetch bound (its code runs once per
+// launch on CUs whose caches do not hold it): a compact loop beats both a register-staged
+// loop with a runtime trip count (one memory round trip per unrolled chunk) and a fully
+// unrolled register-staged fill (16 load + 16 store blocks: 9.0-9.7 k instead of 7.4 k
+// cycles to the first barrier, scripts/k20_prologue.py).  The LDS destination of one wave
+// instruction is 64 consecutive floats (wave-uniform base + lane x 4): the last one may run
+// past na + nb, so dst must have room up to the next multiple of 64 (the lanes there copy
+// the last element).  Requires na + nb >= 1.
+template <int NTH>
+DTP_DEV void lds_dma_fill2(float* dst, const float* A, int na, const float* B, int nb, int tid) {
+  const int n = na + nb;
+  const int wave = tid / kWave, lane = tid - (tid / kWave) * kWave;
+  for (int c = wave * kWave; c < n; c += NTH) {
+    int e = c + lane;
+    e = e < n ? e : n - 1;
+    const float* g = e < na ? A + e : B + (e - na);
+    __builtin_amdgcn_global_load_lds((dtp_gbl_void_t*)const_cast<float*>(g), (dtp_lds_void_t*)(dst + c), 4, 0, 0);
   }
-  DTP_DEV void store(float* __restrict__ dst, int tid) const {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int e = tid + j * NTH;
-      if (e < n) dst[e] = v[j];
-    }
-  }
-};
+}
 
 // error reporting shared by every translation unit (defined in runtime.hip)
 int set_err(int code, const char* msg);

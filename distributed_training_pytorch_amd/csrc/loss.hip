@@ -49,6 +49,65 @@ __global__ __launch_bounds__(kBlock) void mse_bwd_kernel(const float* __restrict
   }
 }
 
+// Two predictions against ONE target (the reference's two models on the same batch,
+// demo_pytorch_lightning.py:27-33: loss_X + loss_Y) in one launch: out = {mse(a1, b),
+// mse(a2, b), their sum} -- the sum in the same fp32 order as torch's `loss_x + loss_y`.
+__global__ __launch_bounds__(kBlock) void mse_pair_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ a2,
+                                                              const float* __restrict__ b, long long n, float inv_n,
+                                                              float* __restrict__ o1, float* __restrict__ o2,
+                                                              float* __restrict__ osum) {
+  __shared__ float part[2][kBlock / kWave];
+  const int tid = threadIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  for (long long i = tid; i < n; i += kBlock) {
+    const float bi = b[i];
+    const float d1 = a1[i] - bi, d2 = a2[i] - bi;
+    s1 = fmaf(d1, d1, s1);
+    s2 = fmaf(d2, d2, s2);
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off, kWave);
+    s2 += __shfl_xor(s2, off, kWave);
+  }
+  if ((tid & (kWave - 1)) == 0) {
+    part[0][tid / kWave] = s1;
+    part[1][tid / kWave] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBlock / kWave; ++w) {
+      t1 += part[0][w];
+      t2 += part[1][w];
+    }
+    const float l1 = t1 * inv_n, l2 = t2 * inv_n;
+    o1[0] = l1;
+    o2[0] = l2;
+    osum[0] = l1 + l2;
+  }
+}
+
+// its backward: ga_k = (g_k + g_sum) 2 (a_k - b) / n for the predictions that need a
+// gradient (g_k / g_sum read on the device; null = 0), gb = -(ga_1 + ga_2) when the target does
+__global__ __launch_bounds__(kBlock) void mse_pair_bwd_kernel(const float* __restrict__ a1, const float* __restrict__ a2,
+                                                              const float* __restrict__ b, const float* __restrict__ g1,
+                                                              const float* __restrict__ g2, const float* __restrict__ gsum,
+                                                              long long n, float scale, float* __restrict__ ga1,
+                                                              float* __restrict__ ga2, float* __restrict__ gb) {
+  const float gt = gsum ? gsum[0] : 0.f;
+  const float gs1 = ((g1 ? g1[0] : 0.f) + gt) * scale;
+  const float gs2 = ((g2 ? g2[0] : 0.f) + gt) * scale;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+    const float bi = b[i];
+    const float d1 = gs1 * (a1[i] - bi), d2 = gs2 * (a2[i] - bi);
+    if (ga1) ga1[i] = d1;
+    if (ga2) ga2[i] = d2;
+    if (gb) gb[i] = -(d1 + d2);
+  }
+}
+
 // the Trainer's replayed batch gather: rows idx of X [nrows, dx] and Y [nrows, dy] into
 // the static batch buffers in ONE launch (torch: one index_select per tensor); indices are
 // clamped into range (an index past the dataset never reads out of bounds)
@@ -102,6 +161,25 @@ int dtp_mse_bwd(const float* a, const float* b, const float* g, long long n, flo
   hipLaunchKernelGGL(dtp::mse_bwd_kernel, dim3(grid), dim3(dtp::kBlock), 0, (hipStream_t)stream, a, b, g, n,
                      2.f / (float)n, ga, gb);
   return dtp::check_launch("mse_bwd_kernel");
+}
+
+int dtp_mse_pair_fwd(const float* a1, const float* a2, const float* b, long long n, float* o1, float* o2,
+                     float* osum, void* stream) {
+  if (!a1 || !a2 || !b || !o1 || !o2 || !osum || n <= 0 || n > dtp_mse_max_elems())
+    return dtp::set_err(-1, "mse_pair_fwd: 1..2^16 elements");
+  hipLaunchKernelGGL(dtp::mse_pair_fwd_kernel, dim3(1), dim3(dtp::kBlock), 0, (hipStream_t)stream, a1, a2, b, n,
+                     1.f / (float)n, o1, o2, osum);
+  return dtp::check_launch("mse_pair_fwd_kernel");
+}
+
+int dtp_mse_pair_bwd(const float* a1, const float* a2, const float* b, const float* g1, const float* g2,
+                     const float* gsum, long long n, float* ga1, float* ga2, float* gb, void* stream) {
+  if (!a1 || !a2 || !b || n <= 0 || (!ga1 && !ga2 && !gb)) return dtp::set_err(-1, "mse_pair_bwd: bad arguments");
+  const long long blocks = (n + dtp::kBlock - 1) / dtp::kBlock;
+  const int grid = (int)(blocks < 1024 ? blocks : 1024);
+  hipLaunchKernelGGL(dtp::mse_pair_bwd_kernel, dim3(grid), dim3(dtp::kBlock), 0, (hipStream_t)stream, a1, a2, b, g1,
+                     g2, gsum, n, 2.f / (float)n, ga1, ga2, gb);
+  return dtp::check_launch("mse_pair_bwd_kernel");
 }
 
 }  // extern "C"

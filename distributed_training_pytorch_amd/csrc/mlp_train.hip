@@ -674,10 +674,6 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
     mr[k] = own ? a.opt_m[(size_t)model * P + p] : 0.f;
     vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
   }
-  // the dataset (inputs then targets) into registers with the other prologue loads; into
-  // LDS after the first wait
-  LdsFill2<kLaneData, NTH> dfill;
-  dfill.load(a.X, smp.n * S::IN, a.Y, smp.n * YD, tid);
   // split-batch publisher (wave 0, DTP_GRP_DIRECT): the dW-tile positions of the parameters of
   // its granules q = tid + 64 j (granule q holds parameters NPT (q / GPT) + 2 (q % GPT), + 1;
   // the last granule is the loss), so it sums them straight from the tiles
@@ -739,7 +735,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   bool gplain = false;
   unsigned long long xwait[2] = {0ull, 0ull};
   for (int e = tid; e < C::pad4(C::LW); e += NTH) sm.wb[e] = 0.f;
-  dfill.store(sm.data, tid);
+  // the dataset (inputs then targets) straight into LDS (LDS-DMA; the first barrier waits)
+  lds_dma_fill2<NTH>(sm.data, a.X, smp.n * S::IN, a.Y, smp.n * YD, tid);
   const int yoff = smp.n * S::IN;
   stamp_launch(18);
   // this wave's staging areas: zero (unwritten rows / columns stay finite), then the

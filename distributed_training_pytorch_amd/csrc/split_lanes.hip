@@ -212,13 +212,12 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
     sl_pos<S, FIRST, LAST>(own ? p : 0, pf[k], pb[k], tp[k]);
     if (!own) pf[k] = pb[k] = C::pad4(C::LW);  // the sink
   }
-  // inputs (first stage) then targets (last stage): issued with the loads above
-  LdsFill2<kSLData, NTH> dfill;
-  dfill.load(a.X, FIRST ? smp.n * S::IN : 0, a.Y, LAST ? smp.n * S::OUT : 0, tid);
   const int t0 = a.step[0];
   for (int e = tid; e < C::pad4(C::LW) + 4; e += NTH) sm.wb[e] = 0.f;
   constexpr int XW = FIRST ? S::IN : 0;
-  dfill.store(sm.data, tid);
+  // inputs (first stage) then targets (last stage), LDS-DMA (the barrier below waits)
+  if constexpr (FIRST || LAST)
+    lds_dma_fill2<NTH>(sm.data, a.X, FIRST ? smp.n * S::IN : 0, a.Y, LAST ? smp.n * S::OUT : 0, tid);
   {  // this wave's staging areas: zero, then the constant-1 bias column of every layer
     float* s0 = &sm.stg[wave][0][0];
     for (int e = lane; e < NL * 2 * C::AREA; e += kWave) s0[e] = 0.f;

@@ -91,3 +91,45 @@ def test_trainer_batch_gather_matches_index_select():
     out = [torch.empty(128, 2, device="cuda"), torch.empty(128, 1, device="cuda")]
     _DevBatch(X, Y, idx).gather_into(idx, out)
     assert torch.equal(out[0], X[idx]) and torch.equal(out[1], Y[idx])
+
+
+def test_mse_loss_pair_cpu_is_torchs():
+    from distributed_training_pytorch_amd.ops.loss import mse_loss_pair
+
+    a1, a2, b = torch.randn(40, 1), torch.randn(40, 1), torch.randn(40, 1)
+    l1, l2, ls = mse_loss_pair(a1, a2, b)
+    assert torch.equal(l1, torch.nn.functional.mse_loss(a1, b)) and torch.equal(ls, l1 + l2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("need2", [True, False])
+def test_mse_loss_pair_fused_matches_two_calls_and_an_add(need2):
+    """The two models' losses on one batch in one launch each way: the same values as two
+    fused MSE calls and an add, and the same gradients (need2=False: the second prediction
+    is frozen, as under the Trainer's optimizer toggling)."""
+    from distributed_training_pytorch_amd.ops.loss import mse_loss_pair
+
+    torch.manual_seed(1)
+    a1 = torch.randn(128, 1, device="cuda", requires_grad=True)
+    a2 = torch.randn(128, 1, device="cuda", requires_grad=need2)
+    b = torch.randn(128, 1, device="cuda")
+    r1 = a1.detach().clone().requires_grad_()
+    r2 = a2.detach().clone().requires_grad_(need2)
+    l1, l2, ls = mse_loss_pair(a1, a2, b)
+    assert "FusedMSEPair" in type(ls.grad_fn).__name__
+    q1, q2 = mse_loss(r1, b), mse_loss(r2, b)
+    qs = q1 + q2
+    assert torch.equal(l1, q1) and torch.equal(l2, q2) and torch.equal(ls, qs)
+    ls.backward()
+    qs.backward()
+    assert torch.equal(a1.grad, r1.grad)
+    if need2:
+        assert torch.equal(a2.grad, r2.grad)
+    # a logged loss used on its own (and the sum) also back-propagates
+    a1.grad = None
+    r1.grad = None
+    l1, _, ls = mse_loss_pair(a1, a2, b)
+    (2.0 * l1 + ls).backward()
+    q1 = mse_loss(r1, b)
+    (2.0 * q1 + (q1 + mse_loss(r2, b))).backward()
+    torch.testing.assert_close(a1.grad, r1.grad, rtol=1e-6, atol=1e-8)
