@@ -34,7 +34,8 @@ class LitToyModel(LightningModule):
         self.lr = lr
 
     def forward(self, x):
-        return self.model_X(x), self.model_Y(x)
+        # both models on the same batch: one fused forward launch on the GPU (models/toy.py)
+        return ToyModel.forward_many([self.model_X, self.model_Y], x)
 
     def training_step(self, batch, batch_idx, optimizer_idx=0):
         x, y = batch

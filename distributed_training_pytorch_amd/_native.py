@@ -116,6 +116,17 @@ class StageArgs(ctypes.Structure):
     ]
 
 
+STAGE_MULTI_MAX = 4
+
+
+class StageMulti(ctypes.Structure):
+    _fields_ = [
+        ("stage", StageArgs * STAGE_MULTI_MAX),
+        ("n", c_int),
+        ("pad_", c_int),
+    ]
+
+
 class SplitStageArgs(ctypes.Structure):
     _fields_ = [
         ("X", c_void_p),
@@ -245,6 +256,7 @@ def _declare(lib):
         "dtp_mlp_train_lanes": (c_int, [P(TrainArgs), c_int, c_int, c_int, c_int, c_int]),
         "dtp_mlp_train_profile_lanes": (c_int, [P(TrainArgs), c_int, c_void_p]),
         "dtp_mlp_stage_fwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
+        "dtp_mlp_stage_fwd_multi": (c_int, [P(StageMulti), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
         "dtp_mse_max_elems": (c_longlong, []),

@@ -95,6 +95,14 @@ struct DtpStageArgs {
 };
 
 int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);
+// up to DTP_STAGE_MULTI_MAX models of one shape forward in ONE launch
+#define DTP_STAGE_MULTI_MAX 4
+struct DtpStageMulti {
+  DtpStageArgs stage[DTP_STAGE_MULTI_MAX];
+  int n;
+  int pad_;
+};
+int dtp_mlp_stage_fwd_multi(const DtpStageMulti* m, int in, int h, int nl, int out, int final_act, void* stream);
 int dtp_mlp_stage_bwd(const DtpStageArgs* a, int in, int h, int nl, int out, int final_act, void* stream);
 
 // ---- persistent layer-split pipeline stage (split_train.hip) ----

@@ -13,8 +13,28 @@ constexpr int kStage = 2 * kStgArr;
 
 // stage forward: one lane per sample, any number of workgroups
 template <class S>
+DTP_DEV void stage_fwd_body(const DtpStageArgs& a, float* sw);
+
+template <class S>
 __global__ __launch_bounds__(kBlock) void mlp_stage_fwd_kernel(DtpStageArgs a) {
   __shared__ __align__(16) float sw[S::pad4(S::LP)];
+  stage_fwd_body<S>(a, sw);
+}
+
+// several models of one shape in ONE launch (blockIdx.y = model): the Trainer demo's two
+// models on the same batch (demo_pytorch_lightning.py: model_X(x), model_Y(x)); the stage
+// arguments come straight from the kernarg segment (indexing the by-value parameter with
+// blockIdx would copy it to scratch)
+template <class S>
+__global__ __launch_bounds__(kBlock) void mlp_stage_fwd_multi_kernel(DtpStageMulti) {
+  __shared__ __align__(16) float sw[S::pad4(S::LP)];
+  const DtpStageMulti* M = (const DtpStageMulti*)__builtin_amdgcn_kernarg_segment_ptr();
+  const DtpStageArgs a = M->stage[blockIdx.y];
+  stage_fwd_body<S>(a, sw);
+}
+
+template <class S>
+DTP_DEV void stage_fwd_body(const DtpStageArgs& a, float* sw) {
   for (int p = threadIdx.x; p < S::P; p += kBlock) lds_store_param<S>(sw, p, a.params[p]);
   __syncthreads();
   const int b = blockIdx.x * kBlock + threadIdx.x;
@@ -139,6 +159,16 @@ int launch_stage_fwd(const DtpStageArgs* a, hipStream_t st) {
 }
 
 template <class S>
+int launch_stage_fwd_multi(const DtpStageMulti* m, hipStream_t st) {
+  int bmax = 0;
+  for (int i = 0; i < m->n; ++i) bmax = m->stage[i].batch > bmax ? m->stage[i].batch : bmax;
+  if (bmax <= 0) return 0;
+  dim3 grid((bmax + dtp::kBlock - 1) / dtp::kBlock, m->n), block(dtp::kBlock);
+  hipLaunchKernelGGL((dtp::mlp_stage_fwd_multi_kernel<S>), grid, block, 0, st, *m);
+  return check_launch("mlp_stage_fwd_multi_kernel");
+}
+
+template <class S>
 int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
   if (a->batch <= 0) return 0;
   // one block reduces deterministically up to 4 chunks; larger batches spread
@@ -183,6 +213,18 @@ int dtp_mlp_stage_fwd(const DtpStageArgs* a, int in, int h, int nl, int out, int
   }
 #define X(I, H, N, O, F) \
   if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_fwd<dtp::Stage<I, H, N, O, F>>(a, st);
+  DTP_STAGE_SHAPES(X)
+#undef X
+  return set_err(-2, "mlp stage shape not instantiated");
+}
+
+int dtp_mlp_stage_fwd_multi(const DtpStageMulti* m, int in, int h, int nl, int out, int final_act, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!m || m->n < 1 || m->n > DTP_STAGE_MULTI_MAX) return set_err(-1, "stage_fwd_multi: 1..4 models");
+  for (int i = 0; i < m->n; ++i)
+    if (m->stage[i].bf16 || m->stage[i].out_peer) return set_err(-1, "stage_fwd_multi: fp32, no peer output");
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_fwd_multi<dtp::Stage<I, H, N, O, F>>(m, st);
   DTP_STAGE_SHAPES(X)
 #undef X
   return set_err(-2, "mlp stage shape not instantiated");

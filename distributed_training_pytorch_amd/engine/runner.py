@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 from ..data.sampler import BatchIndexer, SamplerGeometry
 from ..data.toy_data import ToyData
+from ..ops.gather import gather_rows2
 from ..ops.loss import MSELoss
 from ..ops.optim import OptimConfig
 from ..parallel import comm_util
@@ -301,27 +302,44 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     # captured graph reads this static buffer)
     idx_static = torch.zeros(geom.batch, dtype=torch.int64, device=device)
 
+    # the flat optimizer zeroes the gradient it consumed, so the next step's zero_grad fill
+    # is skipped (reset whenever a capture is abandoned: its zeroing never ran)
+    grads_clean = [False]
+    xb = {}
+
     def step_body(size):
         idx_t = idx_static[:size]
         with timer.phase("data"):
-            x, y = X.index_select(0, idx_t), Y.index_select(0, idx_t)
+            if size not in xb:
+                xb[size] = (torch.empty(size, X.shape[1], device=device), torch.empty(size, Y.shape[1], device=device))
+            x, y = xb[size]
+            gather_rows2(X, Y, idx_t, x, y)  # both tensors in one launch
             if config.loss == "ce":
                 y = y.view(-1).long()
-        bank.zero_grad()
+        if not grads_clean[0]:
+            bank.zero_grad()
         with timer.phase("forward"):
-            ox, oy = ddp(x)
-            lx, ly = lossf(ox, y), lossf(oy, y)
+            ox, oy = ddp(x)  # both models' forwards in one launch (ModelBank.forward)
+            if isinstance(lossf, MSELoss):
+                lx, ly, lsum = lossf.pair(ox, oy, y)  # both losses and their sum in one launch
+            else:
+                lx, ly = lossf(ox, y), lossf(oy, y)
+                lsum = lx + ly
         with timer.phase("backward+allreduce"):
-            (lx + ly).backward()  # independent models: one backward, one bucketed all-reduce
+            lsum.backward()  # independent models: one backward, one bucketed all-reduce
         with timer.phase("optimizer"):
-            opt.step()
+            grads_clean[0] = opt.step(zero_grad=True)
         ring.put_device(lx, ly)
+
+    def _abort():
+        grads_clean[0] = False
+        ddp.reset_hooks()
 
     # hipGraph replay of the whole iteration (engine/graph_step.py) where it can be
     # captured: one rank, xGMI buckets (device-side exchange epochs) or RCCL buckets;
     # not gloo-staged buckets (host-driven)
     graphable = device.type == "cuda" and config.launch != "eager" and not trace_enabled() and ddp.graph_safe()
-    stepper = CapturedStep(step_body, device, enabled=graphable, on_abort=ddp.reset_hooks)
+    stepper = CapturedStep(step_body, device, enabled=graphable, on_abort=_abort)
     for it in range(start, config.iters):
         faults.check(it)
         size = geom.batch_size_at(it)

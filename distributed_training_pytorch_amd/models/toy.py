@@ -91,6 +91,20 @@ class ToyModel(nn.Module):
             self._fused = self.compute_dtype == torch.float32 and self.spec.native_supported()
         return self._fused
 
+    @staticmethod
+    def forward_many(models: list["ToyModel"], x: torch.Tensor) -> tuple:
+        """``tuple(m(x) for m in models)`` for ToyModels of one shape on the same input: on
+        the GPU in fp32 (no autocast) the forwards run as ONE launch (``ops.mlp.
+        fused_mlp_multi``), each backward its own launch; otherwise model by model."""
+        ok = (x.is_cuda and len(models) > 1 and all(m.spec == models[0].spec for m in models)
+              and not torch.is_autocast_enabled("cuda")
+              and all(m.compute_dtype == torch.float32 and m.uses_fused_kernel() for m in models))
+        if not ok:
+            return tuple(m(x) for m in models)
+        from ..ops.mlp import fused_mlp_multi
+
+        return fused_mlp_multi(x.float(), models[0].spec, [list(m.layers.parameters()) for m in models])
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
             cd = self.compute_dtype

@@ -234,6 +234,99 @@ class FusedMLPFunction(torch.autograd.Function):
         return (gin, None, None, *grads)
 
 
+def _stage_param_grads(spec, x, flat, out, saved, grad_out, params, shapes, need_params: bool, need_x: bool):
+    """One model's backward (FusedMLPFunction.backward's body): (grad_in, [param grads]
+    or [None]*n when added in place into persistent flat .grad views)."""
+    target = None
+    if need_params and all(_fused_grad_target(p) is not None for p in params):
+        target = _flat_view_of([p.grad for p in params])
+    gin, gp = stage_backward(x, flat, spec, out, saved if saved.numel() else None, grad_out.float(),
+                             need_grad_in=need_x, grad_params=target)
+    if target is not None:
+        for p in params:
+            _grad_ready(p)
+        return gin, [None] * len(params)
+    if not need_params:
+        return gin, [None] * len(params)
+    grads, o = [], 0
+    for shp in shapes:
+        n = 1
+        for d in shp:
+            n *= d
+        grads.append(gp[o:o + n].view(shp))
+        o += n
+    return gin, grads
+
+
+class FusedMLPMultiFunction(torch.autograd.Function):
+    """(MLP_0(x), ..., MLP_{n-1}(x)) for n models of ONE shape on the same input: the n
+    forwards in ONE launch (``dtp_mlp_stage_fwd_multi``), each backward its own launch,
+    only for the models whose outputs get a gradient and whose parameters want one (the
+    Trainer toggles the other optimizer's models off)."""
+
+    @staticmethod
+    def forward(ctx, x, spec: MlpSpec, n: int, *params):
+        ctx.set_materialize_grads(False)
+        k = len(params) // n
+        groups = [params[i * k:(i + 1) * k] for i in range(n)]
+        x = x.contiguous()
+        dev = x.device
+        B = x.shape[0]
+        m = nat.StageMulti()
+        m.n = n
+        flats, outs, saveds = [], [], []
+        for i, ps in enumerate(groups):
+            flat = _flat_view_of(list(ps))
+            if flat is None:
+                flat = torch.cat([p.detach().reshape(-1) for p in ps])
+            flat = flat.detach()
+            out = torch.empty(B, spec.out_features, device=dev, dtype=torch.float32)
+            saved = torch.empty(B, (spec.n_layers - 1) * spec.hidden, device=dev, dtype=torch.float32) \
+                if spec.n_layers > 1 else torch.empty(0, device=dev)
+            m.stage[i] = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved) if saved.numel() else None,
+                                       None, None, None, None, B, spec.slope, 0, 0)
+            flats.append(flat)
+            outs.append(out)
+            saveds.append(saved)
+        nat.check(nat.require(dev).dtp_mlp_stage_fwd_multi(ctypes.byref(m), *spec.key, nat.stream_ptr()),
+                  "dtp_mlp_stage_fwd_multi")
+        ctx.spec, ctx.n, ctx.k = spec, n, k
+        ctx.groups = groups
+        ctx.shapes = [p.shape for p in groups[0]]
+        ctx.save_for_backward(x, *flats, *outs, *saveds)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        n, k = ctx.n, ctx.k
+        saved_t = ctx.saved_tensors
+        x = saved_t[0]
+        flats, outs, saveds = saved_t[1:1 + n], saved_t[1 + n:1 + 2 * n], saved_t[1 + 2 * n:1 + 3 * n]
+        need = ctx.needs_input_grad
+        gx = None
+        grads = []
+        for i in range(n):
+            g = gouts[i]
+            need_p = any(need[3 + i * k:3 + (i + 1) * k])
+            if g is None or not (need_p or need[0]):
+                grads.extend([None] * k)
+                continue
+            gin, gp = _stage_param_grads(ctx.spec, x, flats[i], outs[i], saveds[i], g, ctx.groups[i], ctx.shapes,
+                                         need_p, need[0])
+            if gin is not None:
+                gx = gin if gx is None else gx + gin
+            grads.extend(gp)
+        return (gx, None, None, *grads)
+
+
+def fused_mlp_multi(x: torch.Tensor, spec: MlpSpec, param_lists: list[list[torch.Tensor]]) -> tuple:
+    """n models of one shape on the same input, forwards in one launch (fp32 GPU);
+    elsewhere the models' forwards one by one."""
+    if x.is_cuda and nat.native_enabled() and spec.native_supported() and 1 <= len(param_lists) <= nat.STAGE_MULTI_MAX:
+        return FusedMLPMultiFunction.apply(x, spec, len(param_lists), *[p for ps in param_lists for p in ps])
+    return tuple(fused_mlp(x, spec, ps) for ps in param_lists)
+
+
 def fused_mlp(x: torch.Tensor, spec: MlpSpec, params: list[torch.Tensor], bf16: bool = False) -> torch.Tensor:
     """The whole MLP as one fused forward and one fused backward kernel.  ``bf16``:
     bf16 compute (bf16 weights / activations / gradients as matmul operands, fp32

@@ -119,19 +119,11 @@ class _DevBatch:
         return [self.X[self.sel], self.Y[self.sel]]
 
     def gather_into(self, idx, out):
-        X, Y, ox, oy = self.X, self.Y, out[0], out[1]
-        if (X.is_cuda and X.dim() == 2 and Y.dim() == 2 and X.dtype == Y.dtype == ox.dtype == oy.dtype == torch.float32
-                and idx.dtype == torch.int64 and all(t.is_contiguous() for t in (X, Y, idx, ox, oy))
-                and ox.shape == (idx.numel(), X.shape[1]) and oy.shape == (idx.numel(), Y.shape[1])
-                and X.shape[0] == Y.shape[0] and nat.native_enabled()):
-            # both tensors in ONE launch (two index_selects otherwise): each launch costs ~4 us in
-            # the replayed step
-            lib = nat.load()
-            nat.check(lib.dtp_gather_rows2(nat.ptr(X), X.shape[1], nat.ptr(Y), Y.shape[1], nat.ptr(idx), idx.numel(),
-                                           X.shape[0], nat.ptr(ox), nat.ptr(oy), nat.stream_ptr()), "dtp_gather_rows2")
-            return
-        torch.index_select(X, 0, idx, out=ox)
-        torch.index_select(Y, 0, idx, out=oy)
+        # both tensors in ONE launch (two index_selects otherwise): each launch costs ~4 us in
+        # the replayed step
+        from ..ops.gather import gather_rows2
+
+        gather_rows2(self.X, self.Y, idx, out[0], out[1])
 
 
 _STEADY_AFTER = 10  # batches excluded from Trainer.steady_time
@@ -833,6 +825,7 @@ class Trainer:
                 model.untoggle_optimizer(-1)
             if ddp is not None:
                 ddp.reset_hooks()
+                ddp._grad_clean = False  # the abandoned capture's gradient zeroing never ran
 
         stepper = CapturedStep(body, self.device, on_abort=abort)
         self._stepper = stepper

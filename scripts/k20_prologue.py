@@ -36,6 +36,7 @@ def one(tr, lib, n, label):
     members_end = [st[8 * k][0][24] for k in range(tr.groups)]
     rec = {
         "launch": label,
+        "prologue_issue": r0[18] - r0[20],      # entry -> every prologue load issued (incl. the status wait)
         "prologue_loads": r0[19] - r0[20],      # entry -> first barrier (params, moments, dataset in LDS)
         "prologue_scatter": r0[22] - r0[19],    # weight scatter into the blocks
         "prologue_adam_tab": r0[23] - r0[22],   # the Adam table rows into LDS

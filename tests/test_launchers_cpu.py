@@ -91,8 +91,15 @@ def _run_torchrun(args, timeout=240):
 
 
 def _summary(out: str) -> dict:
-    line = [l for l in out.splitlines() if "summary:" in l][-1]
-    return eval(line.split("summary:", 1)[1])  # our own printed dict
+    """Rank 0's printed summary dict (our own output).  Two ranks share the pipe, so a line
+    can come out interleaved with another rank's text: take the last one that parses."""
+    lines = [l for l in out.splitlines() if "summary:" in l]
+    for line in reversed(lines):
+        try:
+            return eval(line.split("summary:", 1)[1], {"nan": float("nan"), "inf": float("inf")})
+        except SyntaxError:
+            continue
+    raise AssertionError(f"no parsable summary line in:\n{out[-2000:]}")
 
 
 def test_torchrun_demo_two_ranks():
