@@ -249,7 +249,11 @@ def main():
             from distributed_training_pytorch_amd import _native
 
             torch.cuda.set_stream(_native.cu_masked_stream(dev, [0, 1]))
-        elif a.stream == "pool" and dev.type == "cuda":
+        elif a.stream == "pool" and dev.type == "cuda" and world == 1:
+            # one rank only: ranks that share a GPU (--share-gpu) co-schedule their in-kernel
+            # exchange across processes, and a second queue per process oversubscribes the
+            # hardware queues (the W = 8 rehearsal failed once with it); with several GPUs
+            # the default stream is what every multi-rank run so far used
             torch.cuda.set_stream(torch.cuda.Stream(device=dev))
         X, Y = ds.device_tensors(dev)
         geom = SamplerGeometry(n=n, world=world, rank=rank, batch=a.batch, seed=a.seed)
@@ -269,7 +273,8 @@ def main():
         cfg_desc = {"launch": a.launch, "steps_per_launch": a.steps_per_launch, "comm": runner.comm,
                     "host_cpu": pinned,
                     "sampler": "DistributedSampler order (randperm per epoch)" if a.sampler == "torch"
-                    else "Feistel shuffle", "cu_mask": a.cu_mask, "stream": a.stream,
+                    else "Feistel shuffle", "cu_mask": a.cu_mask,
+                    "stream": "cu_masked" if a.cu_mask == "on" else (a.stream if world == 1 else "default"),
                     # lanes per sample of the fused step (1, or 2 / 4: csrc/mlp_lanes.h for batches <= 128 / 64)
                     "lanes_per_sample": runner.lanes, "waves_per_cu": runner.kernel_waves,
                     # > 1: the split-batch step (csrc/grp_core.h), CUs per model

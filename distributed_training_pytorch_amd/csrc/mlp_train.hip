@@ -576,6 +576,41 @@ DTP_HD constexpr int lane_area(int l) {
   return (Scal<S>::PACK && (l == 0 || l == S::NL - 1)) ? 0 : (l == S::NL - 1 ? 0 : (l == 0 ? 2 : 1));
 }
 
+#ifndef DTP_LANE_OWN
+// 1: the several-lanes kernels' parameter ownership follows the forward blocks' LDS order
+// (lane_own_param) instead of torch order: consecutive lanes then write consecutive LDS
+// words in the post-Adam weight scatter and read consecutive tile slots in the cross-wave
+// gradient sums (torch order puts 5-8 lanes of a 32-lane group on one bank in both).
+// Measured SLOWER at batch 256 (split-batch step, K = 2000, 4 interleaved runs each:
+// 3.351-3.362 vs 3.320-3.331 us/step, profiles/r6_misc/r6j/): off
+#define DTP_LANE_OWN 0
+#endif
+
+// the torch-order parameter of ownership slot s (< P): the forward blocks' LDS order -- a
+// partitioned layer's block is rows r (inputs, then the bias row) of outputs j, the whole
+// last layer's rows j of inputs i (then its bias)
+template <class S>
+DTP_DEV int lane_own_param(int s) {
+  int p = s;
+  static_for<0, S::NL>([&](auto LC) {
+    constexpr int l = decltype(LC)::value;
+    constexpr int I = S::din(l), O = S::dout(l), base = S::gw(l), n = O * (I + 1);
+    if (s >= base && s < base + n) {
+      const int q = s - base;
+      int j, r;
+      if constexpr (l < S::NL - 1) {
+        r = q / O;
+        j = q - r * O;
+      } else {
+        j = q / (I + 1);
+        r = q - j * (I + 1);
+      }
+      p = r < I ? base + j * I + r : S::gb(l) + j;
+    }
+  });
+  return p;
+}
+
 template <class S, int L, int NW, bool GRP = false>
 struct LaneSmem {
   using C = LaneCfg<S, L>;
@@ -663,13 +698,15 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   // ---- prologue (all global reads issued before the first wait, as in mlp_train_kernel)
   float* __restrict__ gp = a.params + (size_t)model * P;
   const SamplerCfg smp = a.smp;
-  int pf[NPT], pb[NPT], tp[NPT];
+  int pf[NPT], pb[NPT], tp[NPT], pown[NPT];
   float pw[NPT], mr[NPT], vr[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int p = NPT * tid + k;
-    lane_pos<C, S>(p < P ? p : 0, pf[k], pb[k], tp[k]);
-    const bool own = p < P;
+    const int s_ = NPT * tid + k;  // ownership slot (the exchanges' payload index)
+    const bool own = s_ < P;
+    const int p = DTP_LANE_OWN ? (own ? lane_own_param<S>(s_) : 0) : s_;
+    pown[k] = p;
+    lane_pos<C, S>(own ? p : 0, pf[k], pb[k], tp[k]);
     pw[k] = own ? gp[p] : 0.f;
     mr[k] = own ? a.opt_m[(size_t)model * P + p] : 0.f;
     vr[k] = (kAdam && own) ? a.opt_v[(size_t)model * P + p] : 0.f;
@@ -1155,8 +1192,8 @@ void mlp_train_lanes_kernel(DtpTrainArgs a) {
   if (!lead) return;  // every member holds the same state: the first writes it back
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int p = NPT * tid + k;
-    if (p < P) {
+    const int p = pown[k];
+    if (NPT * tid + k < P) {
       gp[p] = pw[k];
       a.opt_m[(size_t)model * P + p] = mr[k];
       if (kAdam) a.opt_v[(size_t)model * P + p] = vr[k];
