@@ -135,14 +135,22 @@ DTP_DEV void sl_pos(int p, int& pf, int& pb, int& tp) {
   });
 }
 
-// one lane's slice of a sample's activation / gradient: {ep ^ h(v), v0, v1, v2}
-DTP_DEV void sl_send(void* buf, int idx, unsigned ep, const float (&v)[3], bool local) {
+// one lane's slice of a sample's activation / gradient: {ep ^ h(v), v0, v1, v2}.  local:
+// the reader is on this GPU (sc1 write-through stores; plain: the reader is on this
+// member's XCD, so a plain store that stays in the XCD's L2 is what its sc1 polls read
+// fastest); else system scope (the reader's GPU over xGMI)
+DTP_DEV void sl_send(void* buf, int idx, unsigned ep, const float (&v)[3], bool local, bool plain = false) {
   const uint32_t x0 = __float_as_uint(v[0]), x1 = __float_as_uint(v[1]), x2 = __float_as_uint(v[2]);
   const u32x4 q = {ep ^ xgmi_hash3(x0, x1, x2), x0, x1, x2};
   const __amdgpu_buffer_rsrc_t rs = xgmi_rsrc(buf);
-  if (local) __builtin_amdgcn_raw_buffer_store_b128(q, rs, idx * 16, 0, 16);  // sc1: device scope
+  if (local && plain) __builtin_amdgcn_raw_buffer_store_b128(q, rs, idx * 16, 0, 0);
+  else if (local) __builtin_amdgcn_raw_buffer_store_b128(q, rs, idx * 16, 0, 16);  // sc1: device scope
   else __builtin_amdgcn_raw_buffer_store_b128(q, rs, idx * 16, 0, kSysCoherent);
 }
+
+#ifndef DTP_SL_PLAIN_LINKS
+#define DTP_SL_PLAIN_LINKS 1  // 0: every on-GPU link store write-through (A/B)
+#endif
 
 // poll this lane's granule of epoch ep (bounded; a timeout sets status[0..1])
 DTP_DEV void sl_recv(const void* buf, int idx, unsigned ep, float (&v)[3], bool valid, int* status, int timeout_us,
@@ -296,6 +304,23 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
   const XgmiCtx xc{a.dp_peers, xst, a.dp_world, a.dp_rank, 1, a.timeout_us};
   const unsigned xcc = grp_xcc_id();
   bool gplain = false;
+  // link hello: in its prologue every member stores its XCC id to each on-GPU neighbour
+  // member (one granule past the batch's link granules, tagged with this launch's first
+  // epoch); at the end of step 0 a member reads its readers' ids and, for a reader on its
+  // own XCD, publishes its link granules with plain stores from step 1 on (the line stays
+  // in the shared L2 where the reader's sc1 polls find it; a write-through store drops it
+  // from L2).  Only the writer decides, readers always poll sc1: correct under any
+  // placement, and a hello that has not arrived keeps the write-through form.
+  const int hidx = smp.batch * C::L + gk;
+  const unsigned htag = (unsigned)t0 + 1u;
+  if (DTP_SL_PLAIN_LINKS && tid == 0) {
+    const float hv[3] = {__uint_as_float(xcc), 0.f, 0.f};
+    if constexpr (!FIRST)
+      if (prev_local) sl_send(a.grad_out, hidx, htag, hv, true);
+    if constexpr (!LAST)
+      if (next_local) sl_send(a.act_out, hidx, htag, hv, true);
+  }
+  bool plain_next = false, plain_prev = false;
   // per-lane LDS bases (mlp_train.hip's lanes kernel): the part's slice of the blocks, the
   // sample's slot in a staged operand (+ the part's first row / column), the MFMA reader's
   const float* const wlp = sm.wb + part * NOP;
@@ -441,7 +466,7 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
       // the activation of this member's samples to the next stage, its gradient back
       float s3[3] = {own[NL - 1][0], NO > 1 ? own[NL - 1][NO > 1 ? 1 : 0] : 0.f,
                      NO > 2 ? own[NL - 1][NO > 2 ? 2 : 0] : 0.f};
-      if (valid) sl_send(a.act_out, lidx, ep, s3, next_local);
+      if (valid) sl_send(a.act_out, lidx, ep, s3, next_local, plain_next);
       float go[3];
       sl_recv(a.grad_in, lidx, ep, go, valid, a.status, a.timeout_us, link_dead, next_local);
       static_for<0, NO>([&](auto KC) {
@@ -508,7 +533,7 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
     });
     if constexpr (!FIRST) {  // the stage input's gradient back to the previous stage
       float s3[3] = {dzp[0], NO > 1 ? dzp[NO > 1 ? 1 : 0] : 0.f, NO > 2 ? dzp[NO > 2 ? 2 : 0] : 0.f};
-      if (valid) sl_send(a.grad_out, lidx, ep, s3, prev_local);
+      if (valid) sl_send(a.grad_out, lidx, ep, s3, prev_local, plain_prev);
     }
     // ---------------- the waves' partial tiles -> this member's gradient
     {
@@ -540,6 +565,14 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
       lsum = grp_allreduce_split3<P, NPT, NTH>(gctx, 0, g, lsum, ep, tid, xdead, sm.xg, xcc, gplain, nullptr,
                                                [] {});
       gloss = lsum * inv;
+    }
+    if (DTP_SL_PLAIN_LINKS && it == 0) {  // the readers' hello granules (sent in their prologues)
+      auto hello = [&](const void* buf) -> bool {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(xgmi_rsrc(buf), hidx * 16, 0, 16);
+        return (x.x ^ xgmi_hash3(x.y, x.z, x.w)) == htag && x.y == xcc;
+      };
+      if constexpr (!LAST) plain_next = next_local && hello(a.grad_in);
+      if constexpr (!FIRST) plain_prev = prev_local && hello(a.act_in);
     }
     // the next step's sample and the index of the one after it
     roll(epoch, bi);
@@ -696,6 +729,9 @@ int dtp_split_lanes_launch(const DtpSplitLaunch* L, void* stream) {
     if (a.optim == DTP_MODE_ADAM && !a.opt_v) return set_err(-1, "split lanes: Adam needs opt_v");
     const dtp::SamplerCfg& s = a.smp;
     if (s.batch <= 0 || (s.batch + M - 1) / M > 64) return set_err(-1, "split lanes: batch / members must be <= 64");
+    // the link buffers hold batch x 5 granules (dtp_split_link_bytes, width 10): batch x 4
+    // lane slices, then the members' hello granules
+    if (M > s.batch) return set_err(-1, "split lanes: at most one member per sample");
     const bool first = first_of[id], last = last_of[id];
     if ((first || last) && (s.mode != dtp::SAMPLER_TABLE || !s.perm || s.perm_epochs <= 0 ||
                             (s.perm_epochs & (s.perm_epochs - 1))))

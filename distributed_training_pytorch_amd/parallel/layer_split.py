@@ -517,7 +517,7 @@ class FusedLayerSplit:
             m = int(members)
             if m < need:
                 raise ValueError(f"members={m}: a member runs at most 64 samples (batch {geom.batch} needs >= {need})")
-        if m * max(1, self.world) > 8 or m > 8:
+        if m * max(1, self.world) > 8 or m > 8 or m > geom.batch:
             if members != "auto":
                 raise ValueError(f"members={m} x {self.world} ranks: the exchange serves at most 8")
             return 0
