@@ -259,6 +259,7 @@ def _declare(lib):
         "dtp_mlp_stage_fwd_multi": (c_int, [P(StageMulti), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
+        "dtp_mlp_stage_bwd_opt": (c_int, [P(StageArgs), P(OptArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mse_max_elems": (c_longlong, []),
         "dtp_mse_fwd": (c_int, [c_void_p, c_void_p, c_longlong, c_void_p, c_void_p]),
         "dtp_mse_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_void_p, c_void_p, c_void_p]),
@@ -266,6 +267,9 @@ def _declare(lib):
         "dtp_mse_pair_bwd": (c_int, [c_void_p] * 6 + [c_longlong] + [c_void_p] * 4),
         "dtp_gather_rows2": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_longlong, c_void_p, c_void_p,
                                      c_void_p]),
+        "dtp_gather_rows2_ring": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_longlong,
+                                          c_void_p, c_void_p, c_void_p]),
+        "dtp_gather_ring_max_elems": (c_longlong, []),
         "dtp_randperm_fill": (c_int, [ctypes.c_ulonglong, c_int, c_longlong, c_int, c_void_p, c_int]),
         "dtp_split_launch": (c_int, [P(SplitLaunch), c_void_p]),
         "dtp_split_shape_id": (c_int, [c_int] * 6),

@@ -127,9 +127,48 @@ __global__ __launch_bounds__(kBlock) void gather_rows2_kernel(const float* __res
   }
 }
 
+// the same gather with the batch's indices read from a device-resident epoch ring
+// {cursor, indices of the whole epoch}: batch b = cursor mod steps starts at index
+// b * batch, and the kernel advances the cursor itself.  A replayed step then reads a new
+// batch every replay with nothing refreshed by the host (the per-batch index copy -- a
+// ~3 us blit plus a gap in the replayed stream -- is gone).  ONE workgroup, so every
+// thread's read of the cursor precedes the single write (the barrier orders them).
+__global__ __launch_bounds__(kBlock) void gather_rows2_ring_kernel(const float* __restrict__ X, int dx,
+                                                                   const float* __restrict__ Y, int dy,
+                                                                   long long* __restrict__ ring, int batch, int steps,
+                                                                   int n, long long nrows, float* __restrict__ ox,
+                                                                   float* __restrict__ oy) {
+  const long long cur = ring[0];
+  const long long* __restrict__ idx = ring + 1 + (cur % steps) * (long long)batch;
+  const int w = dx + dy;
+  for (int t = threadIdx.x; t < n * w; t += kBlock) {
+    const int r = t / w, c = t - r * w;
+    long long s = idx[r];
+    s = s < 0 ? 0 : (s >= nrows ? nrows - 1 : s);
+    if (c < dx) ox[(long long)r * dx + c] = X[s * dx + c];
+    else oy[(long long)r * dy + (c - dx)] = Y[s * dy + (c - dx)];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) ring[0] = cur + 1;
+}
+
 }  // namespace dtp
 
 extern "C" {
+
+// one workgroup streams at most this many gathered elements per launch (the toy batches
+// are a few hundred); larger batches take the host-refreshed index path
+long long dtp_gather_ring_max_elems() { return 1ll << 16; }
+
+int dtp_gather_rows2_ring(const float* X, int dx, const float* Y, int dy, long long* ring, int batch, int steps,
+                          int n, long long nrows, float* ox, float* oy, void* stream) {
+  if (!X || !Y || !ring || !ox || !oy || n <= 0 || n > batch || steps <= 0 || dx <= 0 || dy <= 0 || nrows <= 0 ||
+      (long long)n * (dx + dy) > dtp_gather_ring_max_elems())
+    return dtp::set_err(-1, "gather_rows2_ring: bad arguments");
+  hipLaunchKernelGGL(dtp::gather_rows2_ring_kernel, dim3(1), dim3(dtp::kBlock), 0, (hipStream_t)stream, X, dx, Y, dy,
+                     ring, batch, steps, n, nrows, ox, oy);
+  return dtp::check_launch("gather_rows2_ring_kernel");
+}
 
 int dtp_gather_rows2(const float* X, int dx, const float* Y, int dy, const long long* idx, int n, long long nrows,
                      float* ox, float* oy, void* stream) {

@@ -7,6 +7,7 @@
 
 #include "dtp_api.h"
 #include "mlp_core.h"
+#include "optim_core.h"
 
 namespace dtp {
 constexpr int kStage = 2 * kStgArr;
@@ -60,14 +61,22 @@ DTP_DEV void stage_fwd_body(const DtpStageArgs& a, float* sw) {
 }
 
 // stage backward: grid-stride over 256-sample chunks; per-wave MFMA dW tiles,
-// LDS reduction, then one plain store (single block) or float atomics (multi block)
-template <class S, bool WANT_DX>
-__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
+// LDS reduction, then one plain store (single block) or float atomics (multi block).
+// OPT: one block, and the flat optimizer's step over this stage's parameters fused into
+// the store loop (the Trainer's module path: the backward of a toggled model's last
+// autograd node and its optimizer step in ONE launch, ops/mlp.py "param-backward
+// fusion"): the thread that sums dW_p also updates p, m[p], v[p] -- the weights were
+// staged in LDS before, so no wave reads a global weight after it is updated.  The same
+// adam_update / sgd_update as flat_optimizer_kernel: bitwise the unfused pair.
+template <class S, bool WANT_DX, bool OPT>
+DTP_DEV void stage_bwd_body(const DtpStageArgs& a, const DtpOptArgs& o) {
   __shared__ __align__(16) struct {
     float w[S::pad4(S::LP)];
     float stage[4][kStage];
   } sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long t = 0;
+  if constexpr (OPT) t = o.step[0];  // read before the first barrier; advanced at the end by thread 0
   for (int p = tid; p < S::P; p += kBlock) lds_store_param<S>(sm.w, p, a.params[p]);
   __syncthreads();
   f32x4 acc[S::NL];
@@ -108,13 +117,53 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
   __syncthreads();
   store_partial_tiles<S>(&sm.stage[0][0], acc, wave, lane);
   __syncthreads();
-  for (int p = tid; p < S::P; p += kBlock) {
-    const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
-    if (gridDim.x == 1)
-      a.grad_params[p] = a.accumulate ? a.grad_params[p] + g : g;
-    else
-      atomicAdd(&a.grad_params[p], g);
+  if constexpr (OPT) {
+    const bool zg = o.flags & DTP_OPT_ZERO_GRAD;
+    const float gs = o.hp.grad_scale;
+    if (o.kind == DTP_MODE_ADAM) {
+      const AdamScalars sc = adam_scalars(o.hp, t + 1);
+      for (int p = tid; p < S::P; p += kBlock) {
+        const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
+        const float gt = a.accumulate ? a.grad_params[p] + g : g;
+        float w = o.params[p], mi = o.opt_m[p], vi = o.opt_v[p];
+        adam_update(w, mi, vi, gt * gs, sc);
+        o.params[p] = w;
+        o.opt_m[p] = mi;
+        o.opt_v[p] = vi;
+        a.grad_params[p] = zg ? 0.f : gt;
+      }
+    } else {
+      const float lr = (float)o.hp.lr, mom = (float)o.hp.momentum, wd = (float)o.hp.weight_decay;
+      for (int p = tid; p < S::P; p += kBlock) {
+        const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
+        const float gt = a.accumulate ? a.grad_params[p] + g : g;
+        float w = o.params[p], bi = o.opt_m[p];
+        sgd_update(w, bi, gt * gs, lr, mom, wd, t == 0);
+        o.params[p] = w;
+        o.opt_m[p] = bi;
+        a.grad_params[p] = zg ? 0.f : gt;
+      }
+    }
+    if (tid == 0) o.step[0] = (int)(t + 1);
+  } else {
+    for (int p = tid; p < S::P; p += kBlock) {
+      const float g = sum_partial_tiles<S>(&sm.stage[0][0], tile_pos<S>(p), 4);
+      if (gridDim.x == 1)
+        a.grad_params[p] = a.accumulate ? a.grad_params[p] + g : g;
+      else
+        atomicAdd(&a.grad_params[p], g);
+    }
   }
+}
+
+template <class S, bool WANT_DX>
+__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
+  stage_bwd_body<S, WANT_DX, false>(a, DtpOptArgs{});
+}
+
+template <class S>
+__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_opt_kernel(DtpStageArgs a, DtpOptArgs o) {
+  stage_bwd_body<S, false, true>(a, o);
 }
 
 }  // namespace dtp
@@ -182,9 +231,35 @@ int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
     hipLaunchKernelGGL((dtp::mlp_stage_bwd_kernel<S, false>), grid, block, 0, st, *a);
   return check_launch("mlp_stage_bwd_kernel");
 }
+
+// the fused form: one block (batch <= 4 x 256), whole-model fp32 stage, the optimizer's
+// one row exactly this stage's parameters and gradient (checked on the host too)
+template <class S>
+int launch_stage_bwd_opt(const DtpStageArgs* a, const DtpOptArgs* o, hipStream_t st) {
+  if (a->batch <= 0 || a->batch > 4 * dtp::kBlock || a->grad_in || a->bf16 || !a->grad_params)
+    return set_err(-1, "stage_bwd_opt: batch 1..1024, no input gradient, fp32, a gradient span");
+  if (o->n_models != 1 || o->P != S::P || o->params != a->params || o->grad != a->grad_params || o->shadow ||
+      o->loss_log || (o->kind != DTP_MODE_ADAM && o->kind != DTP_MODE_SGD) || !o->opt_m ||
+      (o->kind == DTP_MODE_ADAM && !o->opt_v) || !o->step)
+    return set_err(-1, "stage_bwd_opt: the optimizer row must be this stage's parameters and gradient");
+  hipLaunchKernelGGL((dtp::mlp_stage_bwd_opt_kernel<S>), dim3(1), dim3(dtp::kBlock), 0, st, *a, *o);
+  return check_launch("mlp_stage_bwd_opt_kernel");
+}
 }  // namespace
 
 extern "C" {
+
+int dtp_mlp_stage_bwd_opt(const DtpStageArgs* a, const DtpOptArgs* o, int in, int h, int nl, int out, int final_act,
+                          void* stream) {
+  if (!a || !o) return set_err(-1, "stage_bwd_opt: null arguments");
+  hipStream_t st = (hipStream_t)stream;
+#define X(I, H, N, O, F) \
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd_opt<dtp::Stage<I, H, N, O, F>>(a, o, st);
+  DTP_STAGE_SHAPES(X)
+#undef X
+  return set_err(-2, "mlp stage shape not instantiated");
+}
+
 
 int dtp_mlp_supported_bf16(int in, int h, int nl, int out, int final_act) {
 #define X(I, H, N, O, F) \

@@ -141,6 +141,74 @@ def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool
     return out, saved
 
 
+class ParamBackwardFusion:
+    """A window in which a whole-model stage backward that adds into a persistent flat
+    gradient span (and wants no input gradient) is not launched at once but handed to the
+    next flat optimizer step over exactly that span, which runs both as ONE launch
+    (``csrc/mlp_stage.hip:mlp_stage_bwd_opt_kernel``; ``FlatOptimizer.step(fused=...)``).
+
+    The Trainer's module path opens it around ``loss.backward()`` + the optimizer step
+    at one rank (``Trainer._optimizer_steps``): there nothing reads the gradient in
+    between (no all-reduce), and the toggled model's stage backward is the backward's
+    last launch.  Whatever is still pending when the window closes normally -- a second
+    stage, an optimizer over another span -- is launched as it was; an exception drops it
+    (that backward's gradient is abandoned anyway).  Reference: PL 1.5's per-optimizer
+    backward + step, ``/root/reference/demo_pytorch_lightning.py:27-40``."""
+
+    def __init__(self):
+        self.pending = None
+        self._prev = None
+
+    def __enter__(self):
+        global _FUSION
+        self._prev, _FUSION = _FUSION, self
+        return self
+
+    def __exit__(self, et, ev, tb):
+        global _FUSION
+        _FUSION = self._prev
+        p, self.pending = self.pending, None
+        if p is not None and et is None:
+            p.launch()
+        return False
+
+    def defer(self, pend) -> None:
+        if self.pending is not None:
+            self.pending.launch()
+        self.pending = pend
+
+    def take(self):
+        p, self.pending = self.pending, None
+        return p
+
+
+_FUSION: ParamBackwardFusion | None = None  # read from autograd's device thread too
+
+
+class _PendingStageBackward:
+    """A deferred ``dtp_mlp_stage_bwd`` launch (its operands kept alive until it runs)."""
+
+    __slots__ = ("args", "key", "keep", "device")
+
+    def __init__(self, args, key, keep, device):
+        self.args, self.key, self.keep, self.device = args, key, keep, device
+
+    def matches(self, params: torch.Tensor, grad: torch.Tensor) -> bool:
+        """Whether a one-row optimizer over (params, grad) is exactly this stage's span."""
+        P = self.keep[1].numel()
+        return (params.numel() == P and grad.numel() >= P and params.data_ptr() == self.args.params
+                and grad.data_ptr() == self.args.grad_params)
+
+    def launch(self) -> None:
+        nat.check(nat.require(self.device).dtp_mlp_stage_bwd(ctypes.byref(self.args), *self.key, nat.stream_ptr()),
+                  "dtp_mlp_stage_bwd")
+
+    def launch_with_optimizer(self, opt_args) -> None:
+        nat.check(nat.require(self.device).dtp_mlp_stage_bwd_opt(ctypes.byref(self.args), ctypes.byref(opt_args),
+                                                                 *self.key, nat.stream_ptr()),
+                  "dtp_mlp_stage_bwd_opt")
+
+
 def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: bool = True,
                    grad_params: torch.Tensor | None = None, bf16: bool = False):
     """Native backward of one stage. Returns (grad_in or None, grad_params [P]).
@@ -167,6 +235,12 @@ def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: b
             torch.empty(spec.P, device=dev, dtype=torch.float32)
     a = nat.StageArgs(nat.ptr(x), nat.ptr(flat), nat.ptr(out), nat.ptr(saved), nat.ptr(grad_out),
                       nat.ptr(grad_in), nat.ptr(gp), None, B, spec.slope, int(acc), int(bf16))
+    fus = _FUSION
+    if fus is not None and acc and not need_grad_in and not bf16 and nblk == 1 and grad_out.device == dev \
+            and gp.numel() == spec.P:
+        # handed to the next flat optimizer step over this span (ParamBackwardFusion)
+        fus.defer(_PendingStageBackward(a, spec.key, (x, flat, out, saved, grad_out, gp), dev))
+        return grad_in, gp
     nat.check(lib.dtp_mlp_stage_bwd(ctypes.byref(a), *spec.key, nat.stream_ptr()), "dtp_mlp_stage_bwd")
     return grad_in, gp
 

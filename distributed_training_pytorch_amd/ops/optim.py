@@ -110,14 +110,16 @@ def sgd_update_ref(p: torch.Tensor, buf: torch.Tensor, g: torch.Tensor, first: b
 
 def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: float = 1.0,
                         loss_log=None, loss_scale: float = 1.0, slope: float = 0.01, shadow=None,
-                        zero_grad: bool = False) -> None:
+                        zero_grad: bool = False, fused=None) -> None:
     """One optimizer step over [n_models, P] flat buffers.
 
     ``grad`` is [n_models*P (+ n_models losses)] -- the all-reduced comm buffer;
     ``step`` is the per-model int32 step counter (device or CPU); ``shadow`` (optional,
     bf16 [n_models, >= P], unit column stride) receives the updated parameters rounded
     to bf16 in the same pass, row i at ``shadow[i, :P]``.  ``zero_grad``: the gradient
-    rows are zeroed in the same pass once read (the loss slots are not).
+    rows are zeroed in the same pass once read (the loss slots are not).  ``fused``: a
+    deferred stage backward (``ops.mlp.ParamBackwardFusion``) whose span is exactly this
+    one-row optimizer's: the backward and this step run as one launch.
     """
     n_models, P = params.shape
     if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.dim() != 2 or shadow.shape[0] != n_models
@@ -129,8 +131,13 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
                         nat.ptr(loss_log), 0 if loss_log is None else loss_log.shape[0], n_models, P, cfg.kind,
                         loss_scale, 1 if zero_grad else 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow),
                         0 if shadow is None else shadow.stride(0))
+        if fused is not None:  # the stage backward that produced `grad`, in the same launch
+            fused.launch_with_optimizer(a)
+            return
         nat.check(lib.dtp_flat_optimizer(ctypes.byref(a), nat.stream_ptr()), "dtp_flat_optimizer")
         return
+    if fused is not None:
+        fused.launch()
     g = grad[: n_models * P].view(n_models, P) * grad_scale
     for i in range(n_models):
         t = int(step[i])
@@ -170,23 +177,29 @@ class FlatOptimizer:
         self.slope = slope
 
     @torch.no_grad()
-    def step(self, zero_grad: bool = False) -> bool:
+    def step(self, zero_grad: bool = False, fused=None) -> bool:
         """One step; ``zero_grad``: zero the gradient in the same launch (no separate fill
-        before the next backward).  Returns whether the gradient was zeroed (not when it
-        had to be staged through a copy)."""
+        before the next backward).  ``fused``: a deferred stage backward
+        (``ops.mlp.ParamBackwardFusion.take()``): run in the same launch when its span is
+        exactly this optimizer's one row, else launched first.  Returns whether the
+        gradient was zeroed (not when it had to be staged through a copy)."""
         # the kernel reads grad[i*P : (i+1)*P] only (the loss slots behind them are
         # read only with a loss log), so a contiguous [n, P] gradient is used in place
         n, P = self.params.shape
+        sh = self.shadow
+        fresh = sh is not None and sh._token == sh._current()  # else the next forward re-casts anyway
+        if fused is not None and not (n == 1 and not fresh and self.grad.is_contiguous()
+                                      and fused.matches(self.params, self.grad)):
+            fused.launch()
+            fused = None
         if self.grad.is_contiguous() and self.grad.device == self.params.device:
             buf = self.grad.view(-1)
         else:
             self._buf[: n * P].copy_(self.grad.reshape(-1))
             buf = self._buf
             zero_grad = False
-        sh = self.shadow
-        fresh = sh is not None and sh._token == sh._current()  # else the next forward re-casts anyway
         flat_optimizer_step(self.params, self.m, self.v, self.step_ctr, buf, self.cfg, slope=self.slope,
-                            shadow=sh.buf if fresh else None, zero_grad=zero_grad)
+                            shadow=sh.buf if fresh else None, zero_grad=zero_grad, fused=fused)
         if fresh:
             sh.mark_fresh()
         return zero_grad

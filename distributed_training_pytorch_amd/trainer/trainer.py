@@ -33,6 +33,7 @@ import torch.distributed as dist
 
 from .. import _native as nat
 from ..data.sampler import SamplerGeometry, torch_distributed_indices
+from ..ops.mlp import ParamBackwardFusion
 from ..parallel import comm_util
 from ..parallel.ddp import FlatDDP
 from ..runtime import bootstrap
@@ -84,12 +85,24 @@ class CSVLogger:
 
 
 class _DeviceBatches:
-    """Device-resident replacement for DataLoader(DistributedSampler(ds), batch_size)."""
+    """Device-resident replacement for DataLoader(DistributedSampler(ds), batch_size).
+
+    With ``use_ring()`` (a GPU and batches one workgroup gathers, the Trainer's replayed
+    step) the epoch's indices live in a device ring ``{cursor, indices}`` that the
+    replayed step's gather reads and advances itself (``ops.gather.gather_rows2_ring``):
+    one asynchronous upload from pinned memory per epoch -- none at all while the order
+    does not change (one rank: no shuffle) -- instead of a pageable upload per epoch and
+    an index copy per batch.  ``skip`` (set before iterating) is the number of leading
+    batches the caller will not run (a mid-epoch resume): the cursor starts there."""
 
     def __init__(self, X, Y, batch, world, rank, shuffle, seed=0):
         self.X, self.Y = X, Y
         self.geom = SamplerGeometry(n=X.shape[0], world=world, rank=rank, batch=batch, shuffle=shuffle, seed=seed)
         self.epoch = 0
+        self.skip = 0
+        self.ring = None  # int64 [1 + steps * batch] on the device: cursor, then the epoch's indices
+        self._ring_idx = None  # the indices the ring holds (host copy)
+        self._ring_clean = False  # the last epoch ran to its end: cursor mod steps == 0
 
     def __len__(self):
         return self.geom.steps_per_epoch
@@ -97,23 +110,52 @@ class _DeviceBatches:
     def set_epoch(self, e):
         self.epoch = e
 
+    def use_ring(self) -> bool:
+        from ..ops.gather import ring_gather_ok
+
+        if os.environ.get("DTP_TRAINER_RING", "1") == "0":  # A/B switch: the per-batch index copy
+            return False
+        if self.ring is None and ring_gather_ok(self.X, self.Y, self.geom.batch):
+            self.ring = torch.zeros(1 + len(self) * self.geom.batch, dtype=torch.int64, device=self.X.device)
+        return self.ring is not None
+
     def __iter__(self):
         g = self.geom
         idx = torch_distributed_indices(g.n, g.world, g.rank, self.epoch, g.seed, g.shuffle)
-        idx_t = torch.tensor(idx, device=self.X.device)
+        skip, self.skip = self.skip, 0
+        if self.ring is not None:
+            idx_h = torch.tensor(idx, dtype=torch.int64)
+            if not (self._ring_clean and skip == 0 and self._ring_idx is not None
+                    and torch.equal(idx_h, self._ring_idx)):
+                host = torch.empty(self.ring.numel(), dtype=torch.int64, pin_memory=self.ring.is_cuda)
+                host.zero_()
+                host[0] = skip
+                host[1:1 + idx_h.numel()] = idx_h
+                self.ring.copy_(host, non_blocking=True)  # stream-ordered after the last epoch's gathers
+                self._ring_idx = idx_h
+            idx_t = self.ring[1:1 + idx_h.numel()]
+        else:
+            idx_t = torch.tensor(idx, device=self.X.device)
+        self._ring_clean = False
         for b in range(len(self)):
-            yield _DevBatch(self.X, self.Y, idx_t[b * g.batch:(b + 1) * g.batch])
+            yield _DevBatch(self.X, self.Y, idx_t[b * g.batch:(b + 1) * g.batch], self)
+        self._ring_clean = True
 
 
 class _DevBatch:
     """One batch of ``_DeviceBatches``: the sample indices, gathered on demand.  A
-    replayed step gathers inside its graph (``index_select`` into the static batch
-    buffers), so a batch costs one small index copy on the host side."""
+    replayed step gathers inside its graph into the static batch buffers: from the
+    epoch ring (nothing per batch on the host side) or from a static index buffer the
+    caller refreshes (one small index copy per batch)."""
 
-    __slots__ = ("X", "Y", "sel")
+    __slots__ = ("X", "Y", "sel", "src")
 
-    def __init__(self, X, Y, sel):
-        self.X, self.Y, self.sel = X, Y, sel
+    def __init__(self, X, Y, sel, src):
+        self.X, self.Y, self.sel, self.src = X, Y, sel, src
+
+    @property
+    def ring(self):
+        return self.src.ring
 
     def materialize(self):
         return [self.X[self.sel], self.Y[self.sel]]
@@ -121,9 +163,13 @@ class _DevBatch:
     def gather_into(self, idx, out):
         # both tensors in ONE launch (two index_selects otherwise): each launch costs ~4 us in
         # the replayed step
-        from ..ops.gather import gather_rows2
+        from ..ops.gather import gather_rows2, gather_rows2_ring
 
-        gather_rows2(self.X, self.Y, idx, out[0], out[1])
+        if idx is None:
+            g = self.src.geom
+            gather_rows2_ring(self.X, self.Y, self.src.ring, g.batch, g.steps_per_epoch, out[0], out[1])
+        else:
+            gather_rows2(self.X, self.Y, idx, out[0], out[1])
 
 
 _STEADY_AFTER = 10  # batches excluded from Trainer.steady_time
@@ -210,6 +256,9 @@ class Trainer:
         self.native_optimizers = native_optimizers
         self._flat_opts: list = []
         self._opt_zeroes = False  # the flat optimizers zero the gradient they consume (fit)
+        # the backward's last stage kernel fused with the flat optimizer step (one rank);
+        # DTP_TRAINER_FUSE_OPT=0 launches them separately (A/B)
+        self._fuse_backward_opt = os.environ.get("DTP_TRAINER_FUSE_OPT", "1") != "0"
         self.graph_replays = 0
         self.global_step = 0
         self.current_epoch = 0
@@ -302,6 +351,8 @@ class Trainer:
             owned = [id(p) for f in self._flat_opts for p in f.params]
             self._opt_zeroes = len(owned) == len(set(owned)) and set(owned) == {id(p) for p in ddp._params}
         stepper, static = self._batch_stepper(model, ddp, opts)
+        if stepper is not None and isinstance(loader, _DeviceBatches):
+            loader.use_ring()  # the replayed step reads its batches from the device epoch ring
         logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
         self._log_dir = logger.dir
@@ -324,6 +375,8 @@ class Trainer:
             (self.max_epochs is not None and self.current_epoch >= self.max_epochs)
         try:
             while not done:
+                if isinstance(loader, _DeviceBatches):
+                    loader.skip = self._skip_batches
                 if hasattr(loader, "set_epoch"):
                     loader.set_epoch(self.current_epoch)
                 elif hasattr(getattr(loader, "sampler", None), "set_epoch"):
@@ -339,11 +392,13 @@ class Trainer:
                     if self._refresh_flat_opts() and stepper is not None:
                         stepper.reset()  # the captured optimizer launches hold the old hyperparameters
                     if stepper is not None and (dev is not None or self._static_ok(static, batch)):
-                        if dev is not None:  # indices in, gather inside the replayed step
+                        if dev is not None:  # gather inside the replayed step
                             key = ("idx", dev.sel.shape[0])
                             if key not in static:
-                                static[key] = _StaticBatch(dev.materialize(), dev.sel.clone(), dev)
-                            static[key].idx.copy_(dev.sel)
+                                static[key] = _StaticBatch(dev.materialize(),
+                                                           None if dev.ring is not None else dev.sel.clone(), dev)
+                            if static[key].idx is not None:  # no ring: the batch's indices in
+                                static[key].idx.copy_(dev.sel)
                         else:
                             key = tuple(tuple(b.shape) for b in batch)
                             if key not in static:
@@ -753,15 +808,20 @@ class Trainer:
                 out = model.training_step(batch, batch_idx, oi) if len(opts) > 1 else \
                     model.training_step(batch, batch_idx)
             loss = out["loss"] if isinstance(out, dict) else out
-            # the seed from a cached tensor of ones (autograd's own would be a fill launch per step)
-            loss.backward(self._backward_seed(loss))
             flat = self._flat_opts[oi] if oi < len(self._flat_opts) else None
-            if flat is not None:
-                # the flat kernel zeroes the gradient it consumed: the next zero_grad is free
-                if flat.step(zero_grad=self._opt_zeroes) and ddp is not None:
-                    ddp.mark_grad_clean()
-            else:
-                opt.step()
+            # one rank (nothing reads the gradient between the backward and the step): the
+            # backward's last stage kernel and the flat optimizer step as ONE launch
+            fuse = flat is not None and self._fuse_backward_opt and (ddp is None or ddp.world == 1)
+            with (ParamBackwardFusion() if fuse else contextlib.nullcontext()) as fus:
+                # the seed from a cached tensor of ones (autograd's own would be a fill launch per step)
+                loss.backward(self._backward_seed(loss))
+                if flat is not None:
+                    # the flat kernel zeroes the gradient it consumed: the next zero_grad is free
+                    if flat.step(zero_grad=self._opt_zeroes, fused=fus.take() if fus is not None else None) \
+                            and ddp is not None:
+                        ddp.mark_grad_clean()
+                else:
+                    opt.step()
             if len(opts) > 1:
                 model.untoggle_optimizer(oi)
             model._logged[f"train_loss_opt{oi}"] = loss.detach()
@@ -816,7 +876,7 @@ class Trainer:
 
         def body(key):
             sb = static[key]
-            if sb.idx is not None:
+            if sb.src is not None:  # device batch: the gather is part of the replayed step
                 sb.src.gather_into(sb.idx, sb.tensors)
             self._optimizer_steps(model, ddp, opts, sb.tensors, self._cur_batch_idx)
 
@@ -947,8 +1007,8 @@ class _FlatTorchOptimizer:
         self.cfg = self.flat.cfg = cfg
         return True
 
-    def step(self, zero_grad: bool = False) -> bool:
-        return self.flat.step(zero_grad=zero_grad)
+    def step(self, zero_grad: bool = False, fused=None) -> bool:
+        return self.flat.step(zero_grad=zero_grad, fused=fused)
 
     def export_state(self):
         step = int(self.flat.step_ctr[0].item())

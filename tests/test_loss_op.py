@@ -89,7 +89,7 @@ def test_trainer_batch_gather_matches_index_select():
     Y = torch.randn(512, 1, device="cuda")
     idx = torch.randperm(512, device="cuda")[:128]
     out = [torch.empty(128, 2, device="cuda"), torch.empty(128, 1, device="cuda")]
-    _DevBatch(X, Y, idx).gather_into(idx, out)
+    _DevBatch(X, Y, idx, None).gather_into(idx, out)
     assert torch.equal(out[0], X[idx]) and torch.equal(out[1], Y[idx])
 
 
@@ -133,3 +133,84 @@ def test_mse_loss_pair_fused_matches_two_calls_and_an_add(need2):
     q1 = mse_loss(r1, b)
     (2.0 * q1 + (q1 + mse_loss(r2, b))).backward()
     torch.testing.assert_close(a1.grad, r1.grad, rtol=1e-6, atol=1e-8)
+
+
+def _ring_loader(device, shuffle, world=1, rank=0):
+    from distributed_training_pytorch_amd.trainer.trainer import _DeviceBatches
+
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(500, 2, generator=g).to(device)  # 500 = 3 full batches of 128 + a short one
+    Y = torch.randn(500, 1, generator=g).to(device)
+    loader = _DeviceBatches(X, Y, 128, world, rank, shuffle=shuffle)
+    if device == "cpu":  # the ring's bookkeeping on the host (the one-launch form is GPU only)
+        loader.ring = torch.zeros(1 + len(loader) * 128, dtype=torch.int64)
+    else:
+        assert loader.use_ring()
+    return loader, X, Y
+
+
+def _check_ring_epochs(device, shuffle, world=1):
+    from distributed_training_pytorch_amd.data.sampler import torch_distributed_indices
+
+    loader, X, Y = _ring_loader(device, shuffle, world)
+    uploads = []
+    real_copy = loader.ring.copy_
+    for epoch, skip in ((0, 0), (1, 0), (2, 2), (3, 0)):
+        loader.set_epoch(epoch)
+        loader.skip = skip
+        before = loader._ring_idx
+        ref = torch_distributed_indices(500, world, 0, epoch, 0, shuffle)
+        for b, dev in enumerate(loader):
+            if b < skip:
+                continue
+            n = dev.sel.shape[0]
+            out = [torch.empty(n, 2, device=device), torch.empty(n, 1, device=device)]
+            dev.gather_into(None, out)
+            rows = torch.tensor(ref[b * 128:(b + 1) * 128], device=device)
+            assert torch.equal(out[0], X[rows]) and torch.equal(out[1], Y[rows]), (epoch, b)
+        uploads.append(loader._ring_idx is not before)
+    del real_copy
+    return uploads
+
+
+def test_trainer_epoch_ring_bookkeeping_cpu():
+    """The epoch ring's cursor: every gathered batch advances it, a resumed epoch starts at
+    its skip, and an unchanged order is not uploaded again (host form of the ring gather)."""
+    uploads = _check_ring_epochs("cpu", shuffle=False)
+    # epoch 2 resumes after 2 batches (uploaded with the cursor there); it then runs to its end,
+    # so epoch 3 finds the cursor at a multiple of the epoch and the same order: no upload
+    assert uploads == [True, False, True, False]
+    assert all(_check_ring_epochs("cpu", shuffle=True, world=2))  # a new order every epoch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_trainer_epoch_ring_gather_on_device(shuffle):
+    """The one-launch ring gather (the cursor read and advanced on the device) gives every
+    epoch's batches in DistributedSampler order, short last batch and resume skips included,
+    and a captured gather replays batch after batch with nothing refreshed in between."""
+    from distributed_training_pytorch_amd import _native as nat
+    from distributed_training_pytorch_amd.data.sampler import torch_distributed_indices
+
+    nat.require(torch.device("cuda", 0))
+    _check_ring_epochs("cuda", shuffle, world=2 if shuffle else 1)
+    loader, X, Y = _ring_loader("cuda", False)
+    it = iter(loader)
+    dev = next(it)
+    out = [torch.empty(128, 2, device="cuda"), torch.empty(128, 1, device="cuda")]
+    dev.gather_into(None, out)  # batch 0, eagerly
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=s):
+        dev.gather_into(None, out)
+    ref = torch_distributed_indices(500, 1, 0, 0, 0, False)
+    for k in range(1, 9):  # batches 1, 2, 3, 0, 1, ...: the cursor wraps modulo the 4 steps
+        g.replay()
+        b = k % 4
+        if b == 3:  # the short batch (the Trainer replays its own graph for it)
+            continue
+        rows = torch.tensor(ref[b * 128:(b + 1) * 128], device="cuda")
+        assert torch.equal(out[0], X[rows]) and torch.equal(out[1], Y[rows]), k
+    assert int(loader.ring[0]) == 9

@@ -45,3 +45,49 @@ def test_forward_many_matches_separate_fused_calls(freeze_second):
                 assert p.grad is None
             else:
                 assert torch.equal(p.grad, q.grad)
+
+
+def _train_flat(fuse: bool, opt_name: str, steps: int = 6, batch: int = 200):
+    import contextlib
+
+    from distributed_training_pytorch_amd.ops.loss import mse_loss
+    from distributed_training_pytorch_amd.ops.mlp import ParamBackwardFusion
+    from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(5)
+    m = ToyModel().cuda()
+    ddp = FlatDDP(m)
+    cfg = OptimConfig(name=opt_name, lr=1e-2, momentum=0.9 if opt_name == "sgd" else 0.0)
+    opt = FlatOptimizer(ddp.flat_params, ddp.flat_grad, cfg)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    taken = 0
+    for _ in range(steps):
+        x = torch.randn(batch, 2, device="cuda", generator=g)
+        y = torch.randn(batch, 1, device="cuda", generator=g)
+        ddp.zero_grad()
+        with (ParamBackwardFusion() if fuse else contextlib.nullcontext()) as fus:
+            mse_loss(ddp(x), y).backward()
+            pend = fus.take() if fus is not None else None
+            taken += pend is not None
+            opt.step(zero_grad=True, fused=pend)
+    torch.cuda.synchronize()
+    return [t.detach().clone() for t in (ddp.flat_params, opt.m, opt.v, opt.step_ctr, ddp.flat_grad)], taken
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt_name", ["adam", "sgd"])
+def test_stage_backward_fused_with_flat_optimizer_is_bitwise_the_pair(opt_name):
+    """ParamBackwardFusion: the model's stage backward (adding into its persistent flat
+    gradient) and the flat optimizer step over that span in ONE launch
+    (``mlp_stage_bwd_opt_kernel``) leave parameters, moments, step counter and the
+    (zeroed) gradient bitwise where the two separate launches leave them."""
+    from distributed_training_pytorch_amd import _native as nat
+
+    nat.require(torch.device("cuda", 0))
+    ref, n0 = _train_flat(False, opt_name)
+    got, n1 = _train_flat(True, opt_name)
+    assert n0 == 0 and n1 == 6  # every step fused
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    assert int(got[3][0]) == 6 and not got[4].any()
