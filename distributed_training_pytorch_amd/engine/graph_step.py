@@ -43,7 +43,10 @@ class CapturedStep:
         self.replays = 0
         self.fallback_reason: str | None = None
 
-    def run(self, key: Hashable = None) -> None:
+    def run(self, key: Hashable = None, warm_key: Hashable = None) -> None:
+        """Replay ``key``'s graph (capturing it first).  ``warm_key``: the eager warm-up
+        runs are counted per ``warm_key`` instead (several graph copies of one body:
+        the first copy's warm-up serves them all)."""
         g = self._graphs.get(key)
         if g is not None and g is not False:
             g.replay()
@@ -52,7 +55,8 @@ class CapturedStep:
         if g is False or not self.enabled:
             self.body(key)
             return
-        n = self._seen.get(key, 0)
+        wk = key if warm_key is None else warm_key
+        n = self._seen.get(wk, 0)
         cur = torch.cuda.current_stream(self.device)
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(cur)
@@ -60,7 +64,7 @@ class CapturedStep:
             with torch.cuda.stream(side):
                 self.body(key)
             cur.wait_stream(side)
-            self._seen[key] = n + 1
+            self._seen[wk] = n + 1
             return
         graph = torch.cuda.CUDAGraph()
         try:

@@ -182,22 +182,33 @@ class _MetricRing:
     reference (``log_every_n_steps=0.03125``).  Reducing and printing each of those on
     the host costs a collective and a device->host sync per batch, which would stall
     the replayed step after every batch.  Instead each logged step's values are stacked
-    into a device row (the graph outputs are copied before the next replay overwrites
-    them), and every ``rows`` logged steps -- and before a checkpoint and at the end of
-    ``fit`` -- the block is averaged over ranks with ONE all-reduce, copied to the host
-    once and written to ``metrics.csv`` row by row.  ``callback_metrics`` is the last
-    row of the newest block, so it trails the live step by less than ``rows`` logged
-    steps during training and is exact after ``fit``."""
+    into a device row, and every ``rows`` logged steps -- and before a checkpoint and at
+    the end of ``fit`` -- the block is averaged over ranks with ONE all-reduce, copied to
+    the host once and written to ``metrics.csv`` row by row -- without a device sync:
+    a block's rows are written once its copy has arrived (``flush``).
+    ``callback_metrics`` is the last row of the newest written block, so it trails the
+    live step by less than 2 x ``rows`` logged steps during training and is exact after
+    ``fit``.
 
-    def __init__(self, trainer, logger, rows: int = 64):
+    The stack itself is deferred: a logged step's tensors are kept (``pending``) until
+    ``defer`` steps are waiting or the graph copy that wrote them (``owner``) is about to
+    be replayed again (``release``), then all waiting rows are stacked in ONE launch --
+    with the Trainer's ``graph_copies`` replayed graphs per batch shape, one stack per
+    ``graph_copies`` batches instead of one per batch."""
+
+    def __init__(self, trainer, logger, rows: int = 64, defer: int = 1):
         self.tr = trainer
         self.logger = logger
         self.rows = rows
+        self.defer = max(1, int(defer))
         self.buf = None
         self.keys: list = []
         self.steps: list = []
+        self.pending: list = []  # (step, [tensors], owner)
+        self._inflight: list = []  # (event, pinned rows, steps, keys) copied but not yet written
+        self._sync_flush = os.environ.get("DTP_TRAINER_SYNC_FLUSH", "0") == "1"  # A/B: the blocking flush
 
-    def push(self, step: int, logged: dict) -> None:
+    def push(self, step: int, logged: dict, owner=None) -> None:
         keys = list(logged.keys())
         if not keys:
             return
@@ -205,24 +216,57 @@ class _MetricRing:
             self.flush()
             self.keys = keys
             self.buf = torch.empty(self.rows, len(keys), dtype=torch.float32, device=self.tr.device)
-        torch.stack([v.detach().float().reshape(()) for v in logged.values()], out=self.buf[len(self.steps)])
-        self.steps.append(step)
-        if len(self.steps) == self.rows:
-            self.flush()
+        self.pending.append((step, [v.detach() for v in logged.values()], owner))
+        if len(self.pending) >= self.defer or len(self.steps) + len(self.pending) >= self.rows:
+            self._stack_pending()
+            if len(self.steps) == self.rows:
+                self.flush(wait=self._sync_flush)
 
-    def flush(self) -> None:
-        if not self.steps:
+    def release(self, owner) -> None:
+        """``owner``'s output tensors are about to be overwritten: stack what waits."""
+        if any(o == owner for _, _, o in self.pending):
+            self._stack_pending()
+
+    def _stack_pending(self) -> None:
+        if not self.pending:
             return
-        block = self.buf[:len(self.steps)]
-        if self.tr.world_size > 1:
-            comm_util.all_reduce_(block)
-            block /= self.tr.world_size
-        rows = block.tolist()
-        for step, vals in zip(self.steps, rows):
-            self.logger.log(step, dict(zip(self.keys, vals)))
-        self.logger.flush()
-        self.tr.callback_metrics = dict(zip(self.keys, rows[-1]))
-        self.steps = []
+        n0, k = len(self.steps), len(self.pending)
+        vals = [v.float().reshape(()) for _, vs, _ in self.pending for v in vs]
+        torch.stack(vals, out=self.buf[n0:n0 + k].view(-1))
+        self.steps.extend(st for st, _, _ in self.pending)
+        self.pending = []
+
+    def flush(self, wait: bool = True) -> None:
+        """Reduce the block and start its copy to the host.  ``wait=False`` (the periodic
+        flush inside training): no device sync -- the copy lands in pinned memory behind
+        the queued batches and its rows are written at a later flush once it has arrived,
+        so the replayed steps queued behind it keep the GPU busy while the host writes
+        CSV.  ``wait=True`` (checkpoint, end of ``fit``): everything written now."""
+        self._stack_pending()
+        if self.steps:
+            block = self.buf[:len(self.steps)]
+            if self.tr.world_size > 1:
+                comm_util.all_reduce_(block)
+                block /= self.tr.world_size
+            ev = None
+            if block.is_cuda:
+                host = torch.empty(block.shape, dtype=block.dtype, pin_memory=True)
+                host.copy_(block, non_blocking=True)  # stream-ordered before the rows are reused
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host = block.clone()
+            self._inflight.append((ev, host, self.steps, self.keys))
+            self.steps = []
+        while self._inflight and (wait or self._inflight[0][0] is None or self._inflight[0][0].query()):
+            ev, host, steps, keys = self._inflight.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            rows = host.tolist()
+            for step, vals in zip(steps, rows):
+                self.logger.log(step, dict(zip(keys, vals)))
+            self.logger.flush()
+            self.tr.callback_metrics = dict(zip(keys, rows[-1]))
 
 
 class Trainer:
@@ -231,7 +275,7 @@ class Trainer:
                  log_every_n_steps: float = 50, default_root_dir: str | None = None,
                  enable_checkpointing: bool = True, enable_progress_bar: bool = True, seed: int | None = None,
                  use_graphs: bool = True, native_optimizers: bool = True, every_n_train_steps: int = 0,
-                 engine: str = "auto", **unused):
+                 engine: str = "auto", graph_copies: int | None = None, **unused):
         if precision in (32, "32", "32-true"):
             self.autocast_dtype = None
         elif precision in ("bf16", "bf16-mixed"):
@@ -252,6 +296,12 @@ class Trainer:
         self.enable_progress_bar = enable_progress_bar
         self.seed = seed
         self.use_graphs = use_graphs  # replay each batch's optimizer steps as a hipGraph (GPU)
+        # graphs captured per batch shape, replayed in turn: each keeps its logged outputs
+        # until its next replay, so the metric rows are stacked once per `graph_copies` batches
+        # (default 4; DTP_TRAINER_GRAPH_COPIES overrides the default, for A/Bs)
+        if graph_copies is None:
+            graph_copies = int(os.environ.get("DTP_TRAINER_GRAPH_COPIES", "4"))
+        self.graph_copies = max(1, int(graph_copies))
         # run a plain torch Adam/SGD over a flat-buffer span as ONE flat-optimizer kernel (GPU)
         self.native_optimizers = native_optimizers
         self._flat_opts: list = []
@@ -356,7 +406,8 @@ class Trainer:
         logged_by_key: dict = {}
         logger = CSVLogger(self.root, self.global_rank)
         self._log_dir = logger.dir
-        metrics = _MetricRing(self, logger)
+        copies = self.graph_copies if stepper is not None else 1
+        metrics = _MetricRing(self, logger, defer=copies)
         pbar = None
         if self.enable_progress_bar and self.global_rank == 0:
             try:
@@ -370,7 +421,9 @@ class Trainer:
         t0 = time.perf_counter()
         # steady-state clock: from the end of batch _STEADY_AFTER on (warm-up batches,
         # graph capture and first kernel loads excluded); synchronised at both ends
-        self.steady_time, self.steady_steps, steady_t0, steady_from = None, 0, None, self.global_step + _STEADY_AFTER
+        # (the warm-up runs and every graph copy's capture come first)
+        self.steady_time, self.steady_steps, steady_t0 = None, 0, None
+        steady_from = self.global_step + max(_STEADY_AFTER, copies + 6)
         done = 0 <= self.max_steps <= self.global_step or \
             (self.max_epochs is not None and self.current_epoch >= self.max_epochs)
         try:
@@ -406,15 +459,22 @@ class Trainer:
                             for dst, src in zip(static[key].tensors, batch):
                                 dst.copy_(src)
                         self._cur_batch_idx = batch_idx  # read by the body only while capturing
-                        replay = stepper.is_captured(key)
-                        stepper.run(key)
-                        # logged tensors of a replay are that key's graph outputs (refreshed in place)
+                        # several graph copies per batch shape, replayed in turn: a copy's
+                        # logged outputs stay valid until its next replay (_MetricRing.release)
+                        gkey = (key, self.global_step % copies)
+                        replay = stepper.is_captured(gkey)
                         if replay:
-                            model._logged.update(logged_by_key[key])
+                            metrics.release(gkey)
+                        stepper.run(gkey, warm_key=key)
+                        # logged tensors of a replay are that copy's graph outputs (refreshed in place)
+                        if replay:
+                            model._logged.update(logged_by_key[gkey])
                         else:
-                            logged_by_key[key] = dict(model._logged)
+                            logged_by_key[gkey] = dict(model._logged)
+                        owner = gkey
                     else:
                         self._optimizer_steps(model, ddp, opts, batch, batch_idx)
+                        owner = None
                     self.global_step += 1  # PL 1.5: once per batch, whatever the optimizer count
                     if self.global_step == steady_from:
                         if self.device.type == "cuda":
@@ -422,7 +482,7 @@ class Trainer:
                         steady_t0 = time.perf_counter()
                     self._batch_in_epoch = batch_idx + 1
                     if self.global_step % self.log_every_n_steps == 0:
-                        metrics.push(self.global_step, model._logged)
+                        metrics.push(self.global_step, model._logged, owner)
                     if pbar is not None:
                         pbar.update(1)
                     if self.every_n_train_steps and self.global_step % self.every_n_train_steps == 0:
@@ -874,8 +934,8 @@ class Trainer:
 
         static: dict = {}
 
-        def body(key):
-            sb = static[key]
+        def body(gkey):
+            sb = static[gkey[0]]  # (batch shape, graph copy)
             if sb.src is not None:  # device batch: the gather is part of the replayed step
                 sb.src.gather_into(sb.idx, sb.tensors)
             self._optimizer_steps(model, ddp, opts, sb.tensors, self._cur_batch_idx)

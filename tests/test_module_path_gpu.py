@@ -91,3 +91,45 @@ def test_stage_backward_fused_with_flat_optimizer_is_bitwise_the_pair(opt_name):
     for a, b in zip(ref, got):
         assert torch.equal(a, b)
     assert int(got[3][0]) == 6 and not got[4].any()
+
+
+def _fit_lit(root, copies, graphs=True, steps=23, batch=96):
+    import csv
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from demo_pytorch_lightning import LitToyModel
+    from distributed_training_pytorch_amd.data.toy_data import ToyData
+    from distributed_training_pytorch_amd.trainer import Trainer
+
+    torch.manual_seed(0)
+    dl = torch.utils.data.DataLoader(ToyData(seed=0), batch_size=batch)
+    model = LitToyModel()
+    tr = Trainer(gpus=1, max_steps=steps, accelerator="gpu", log_every_n_steps=1, default_root_dir=str(root),
+                 enable_progress_bar=False, use_graphs=graphs, enable_checkpointing=False, engine="module",
+                 graph_copies=copies)
+    tr.fit(model, dl)
+    with open(os.path.join(tr._log_dir, "metrics.csv")) as f:
+        rows = list(csv.DictReader(f))
+    return {k: v.cpu() for k, v in model.state_dict().items()}, rows, tr.graph_replays, tr.callback_metrics
+
+
+@pytest.mark.gpu
+def test_trainer_graph_copies_log_every_step_like_eager(tmp_path):
+    """Several graph copies per batch shape (the metric rows stacked once per copies
+    batches, each copy's logged outputs kept until its next replay): the same weights and
+    the same metrics.csv, row for row, as one copy and as eager batches -- batch 96 of
+    512 samples gives a short last batch (a second batch shape) every epoch."""
+    from distributed_training_pytorch_amd import _native as nat
+
+    nat.require(torch.device("cuda", 0))
+    s4, r4, n4, c4 = _fit_lit(tmp_path / "c4", 4)
+    s1, r1, n1, c1 = _fit_lit(tmp_path / "c1", 1)
+    se, re_, ne, ce = _fit_lit(tmp_path / "e", 1, graphs=False)
+    assert ne == 0 and n1 >= 15 and n4 >= 10, (n1, n4)
+    assert len(r4) == len(r1) == len(re_) == 23
+    assert r4 == r1 == re_
+    assert c4 == c1 == ce
+    for k in s1:
+        assert torch.equal(s4[k], s1[k]) and torch.equal(s1[k], se[k]), k
