@@ -259,11 +259,12 @@ def _declare(lib):
         "dtp_mlp_stage_fwd_multi": (c_int, [P(StageMulti), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mlp_stage_bwd": (c_int, [P(StageArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_flat_optimizer": (c_int, [P(OptArgs), c_void_p]),
-        "dtp_mlp_stage_bwd_opt": (c_int, [P(StageArgs), P(OptArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
+        "dtp_mlp_stage_bwd_opt": (c_int, [P(StageMulti), P(OptArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]),
         "dtp_mse_max_elems": (c_longlong, []),
         "dtp_mse_fwd": (c_int, [c_void_p, c_void_p, c_longlong, c_void_p, c_void_p]),
         "dtp_mse_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_void_p, c_void_p, c_void_p]),
-        "dtp_mse_pair_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_void_p, c_void_p, c_void_p, c_void_p]),
+        "dtp_mse_pair_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_int, c_void_p]),
         "dtp_mse_pair_bwd": (c_int, [c_void_p] * 6 + [c_longlong] + [c_void_p] * 4),
         "dtp_gather_rows2": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_longlong, c_void_p, c_void_p,
                                      c_void_p]),

@@ -133,7 +133,8 @@ struct DtpSplitStageArgs {
   int dp_world;
   int dp_rank;
   int optim;              // DTP_MODE_ADAM or DTP_MODE_SGD
-  int link_local;         // bit 0: the previous stage, bit 1: the next stage is on this GPU
+  int link_local;         // bit 0: the previous stage, bit 1: the next stage is on this GPU;
+                          // bit 2: every neighbour stage runs in this launch (split_lanes.hip plain links)
                           // (device-scope link: plain device memory, sc1); else system scope
   dtp::SamplerCfg smp;
   DtpHyper hp;            // grad_scale = 1 / dp_world

@@ -55,7 +55,8 @@ __global__ __launch_bounds__(kBlock) void mse_bwd_kernel(const float* __restrict
 __global__ __launch_bounds__(kBlock) void mse_pair_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ a2,
                                                               const float* __restrict__ b, long long n, float inv_n,
                                                               float* __restrict__ o1, float* __restrict__ o2,
-                                                              float* __restrict__ osum) {
+                                                              float* __restrict__ osum, float* __restrict__ ring,
+                                                              long long* __restrict__ slot, int width) {
   __shared__ float part[2][kBlock / kWave];
   const int tid = threadIdx.x;
   float s1 = 0.f, s2 = 0.f;
@@ -86,6 +87,12 @@ __global__ __launch_bounds__(kBlock) void mse_pair_fwd_kernel(const float* __res
     o1[0] = l1;
     o2[0] = l2;
     osum[0] = l1 + l2;
+    if (ring) {  // the engine's device loss log (utils/logging.py LossRing): row[slot] = (l1, l2); slot += 1
+      const long long sl = slot[0];
+      ring[sl * width] = l1;
+      ring[sl * width + 1] = l2;
+      slot[0] = sl + 1;
+    }
   }
 }
 
@@ -202,12 +209,15 @@ int dtp_mse_bwd(const float* a, const float* b, const float* g, long long n, flo
   return dtp::check_launch("mse_bwd_kernel");
 }
 
+// ring / slot (nullable): also append (loss1, loss2) to a device loss log of `width` >= 2
+// floats per row at row slot[0], and advance slot[0] (the caller sizes the log)
 int dtp_mse_pair_fwd(const float* a1, const float* a2, const float* b, long long n, float* o1, float* o2,
-                     float* osum, void* stream) {
+                     float* osum, float* ring, long long* slot, int width, void* stream) {
   if (!a1 || !a2 || !b || !o1 || !o2 || !osum || n <= 0 || n > dtp_mse_max_elems())
     return dtp::set_err(-1, "mse_pair_fwd: 1..2^16 elements");
+  if (ring && (!slot || width < 2)) return dtp::set_err(-1, "mse_pair_fwd: a loss log needs a slot and width >= 2");
   hipLaunchKernelGGL(dtp::mse_pair_fwd_kernel, dim3(1), dim3(dtp::kBlock), 0, (hipStream_t)stream, a1, a2, b, n,
-                     1.f / (float)n, o1, o2, osum);
+                     1.f / (float)n, o1, o2, osum, ring, slot, width);
   return dtp::check_launch("mse_pair_fwd_kernel");
 }
 

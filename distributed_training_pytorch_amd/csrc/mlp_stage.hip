@@ -161,8 +161,22 @@ __global__ __launch_bounds__(kBlock) void mlp_stage_bwd_kernel(DtpStageArgs a) {
   stage_bwd_body<S, WANT_DX, false>(a, DtpOptArgs{});
 }
 
+// several models of one shape (blockIdx.y = model): model y's stage backward and the
+// optimizer's row y in one block -- the module engine's ModelBank (both models' backwards
+// and their one flat Adam: 3 launches -> 1).  Arguments from the kernarg segment, as in
+// the forward's multi kernel.
 template <class S>
-__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_opt_kernel(DtpStageArgs a, DtpOptArgs o) {
+__global__ __launch_bounds__(kBlock) void mlp_stage_bwd_opt_kernel(DtpStageMulti, DtpOptArgs O) {
+  const DtpStageMulti* M = (const DtpStageMulti*)__builtin_amdgcn_kernarg_segment_ptr();  // the first argument
+  const int y = blockIdx.y;
+  const DtpStageArgs a = M->stage[y];
+  DtpOptArgs o = O;
+  const size_t off = (size_t)y * o.P;
+  o.params += off;
+  o.opt_m += off;
+  if (o.opt_v) o.opt_v += off;
+  o.step += y;
+  o.grad += off;
   stage_bwd_body<S, false, true>(a, o);
 }
 
@@ -232,34 +246,37 @@ int launch_stage_bwd(const DtpStageArgs* a, hipStream_t st) {
   return check_launch("mlp_stage_bwd_kernel");
 }
 
-// the fused form: one block (batch <= 4 x 256), whole-model fp32 stage, the optimizer's
-// one row exactly this stage's parameters and gradient (checked on the host too)
+// the fused form: one block per model (batch <= 4 x 256), whole-model fp32 stages, the
+// optimizer's row i exactly model i's parameters and gradient (checked on the host too)
 template <class S>
-int launch_stage_bwd_opt(const DtpStageArgs* a, const DtpOptArgs* o, hipStream_t st) {
-  if (a->batch <= 0 || a->batch > 4 * dtp::kBlock || a->grad_in || a->bf16 || !a->grad_params)
-    return set_err(-1, "stage_bwd_opt: batch 1..1024, no input gradient, fp32, a gradient span");
-  if (o->n_models != 1 || o->P != S::P || o->params != a->params || o->grad != a->grad_params || o->shadow ||
-      o->loss_log || (o->kind != DTP_MODE_ADAM && o->kind != DTP_MODE_SGD) || !o->opt_m ||
-      (o->kind == DTP_MODE_ADAM && !o->opt_v) || !o->step)
-    return set_err(-1, "stage_bwd_opt: the optimizer row must be this stage's parameters and gradient");
-  hipLaunchKernelGGL((dtp::mlp_stage_bwd_opt_kernel<S>), dim3(1), dim3(dtp::kBlock), 0, st, *a, *o);
+int launch_stage_bwd_opt(const DtpStageMulti* m, const DtpOptArgs* o, hipStream_t st) {
+  if (m->n < 1 || m->n > DTP_STAGE_MULTI_MAX || o->n_models != m->n || o->P != S::P || o->shadow || o->loss_log ||
+      (o->kind != DTP_MODE_ADAM && o->kind != DTP_MODE_SGD) || !o->opt_m || (o->kind == DTP_MODE_ADAM && !o->opt_v) ||
+      !o->step)
+    return set_err(-1, "stage_bwd_opt: the optimizer rows must be the stages' parameters and gradients");
+  for (int i = 0; i < m->n; ++i) {
+    const DtpStageArgs& a = m->stage[i];
+    if (a.batch <= 0 || a.batch > 4 * dtp::kBlock || a.grad_in || a.bf16 || !a.grad_params ||
+        o->params + (size_t)i * S::P != a.params || o->grad + (size_t)i * S::P != a.grad_params)
+      return set_err(-1, "stage_bwd_opt: batch 1..1024, no input gradient, fp32, row i = stage i");
+  }
+  hipLaunchKernelGGL((dtp::mlp_stage_bwd_opt_kernel<S>), dim3(1, m->n), dim3(dtp::kBlock), 0, st, *m, *o);
   return check_launch("mlp_stage_bwd_opt_kernel");
 }
 }  // namespace
 
 extern "C" {
 
-int dtp_mlp_stage_bwd_opt(const DtpStageArgs* a, const DtpOptArgs* o, int in, int h, int nl, int out, int final_act,
+int dtp_mlp_stage_bwd_opt(const DtpStageMulti* m, const DtpOptArgs* o, int in, int h, int nl, int out, int final_act,
                           void* stream) {
-  if (!a || !o) return set_err(-1, "stage_bwd_opt: null arguments");
+  if (!m || !o) return set_err(-1, "stage_bwd_opt: null arguments");
   hipStream_t st = (hipStream_t)stream;
 #define X(I, H, N, O, F) \
-  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd_opt<dtp::Stage<I, H, N, O, F>>(a, o, st);
+  if (in == I && h == H && nl == N && out == O && (bool)final_act == F) return launch_stage_bwd_opt<dtp::Stage<I, H, N, O, F>>(m, o, st);
   DTP_STAGE_SHAPES(X)
 #undef X
   return set_err(-2, "mlp stage shape not instantiated");
 }
-
 
 int dtp_mlp_supported_bf16(int in, int h, int nl, int out, int final_act) {
 #define X(I, H, N, O, F) \

@@ -313,7 +313,8 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
   // placement, and a hello that has not arrived keeps the write-through form.
   const int hidx = smp.batch * C::L + gk;
   const unsigned htag = (unsigned)t0 + 1u;
-  if (DTP_SL_PLAIN_LINKS && tid == 0) {
+  const bool plain_ok = DTP_SL_PLAIN_LINKS && (a.link_local & 4);  // neighbours in this launch
+  if (plain_ok && tid == 0) {
     const float hv[3] = {__uint_as_float(xcc), 0.f, 0.f};
     if constexpr (!FIRST)
       if (prev_local) sl_send(a.grad_out, hidx, htag, hv, true);
@@ -566,7 +567,7 @@ DTP_DEV void split_lanes_body(const DtpSplitStageArgs& a, unsigned char* smem, i
                                                [] {});
       gloss = lsum * inv;
     }
-    if (DTP_SL_PLAIN_LINKS && it == 0) {  // the readers' hello granules (sent in their prologues)
+    if (plain_ok && it == 0) {  // the readers' hello granules (sent in their prologues)
       auto hello = [&](const void* buf) -> bool {
         const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(xgmi_rsrc(buf), hidx * 16, 0, 16);
         return (x.x ^ xgmi_hash3(x.y, x.z, x.w)) == htag && x.y == xcc;

@@ -250,6 +250,28 @@ class BatchIndexer:
                 self._cfg = geom.to_native()
                 self._buf = torch.empty(self.block, geom.batch, dtype=torch.int32, device=self.device)
 
+    def can_fill_epoch(self) -> bool:
+        """Whether ``epoch_into`` is available (the device permutation ring or the host
+        epoch list; not the native per-step sampler's blocks)."""
+        return self._native is None
+
+    def epoch_into(self, epoch: int, out: torch.Tensor) -> None:
+        """Epoch ``epoch``'s per-rank indices (``num_samples`` int64) into ``out`` on the
+        current stream -- the module engine's device epoch ring, which its replayed gather
+        reads with a cursor (``ops.gather.gather_rows2_ring``)."""
+        if self._ring is not None:
+            self._ring.ensure(epoch, epoch)
+            perm = self._ring.table[epoch & (self._ring.E - 1)]
+            out.copy_(perm.index_select(0, self._q))
+            return
+        if self.exact:
+            host = torch.tensor(self._stream.epoch_list(epoch), dtype=torch.int64)
+        else:
+            host = torch.from_numpy(self.geom.epoch_indices(epoch))
+        if out.is_cuda:
+            host = host.pin_memory()
+        out.copy_(host, non_blocking=True)
+
     def __call__(self, t: int) -> torch.Tensor:
         epoch, start, size = self.geom.batch_pos(t)
         if self._native is not None:

@@ -17,6 +17,7 @@ Engines (``--engine``):
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 import socket
@@ -27,8 +28,9 @@ import torch.distributed as dist
 
 from ..data.sampler import BatchIndexer, SamplerGeometry
 from ..data.toy_data import ToyData
-from ..ops.gather import gather_rows2
+from ..ops.gather import gather_rows2, gather_rows2_ring, ring_gather_ok
 from ..ops.loss import MSELoss
+from ..ops.mlp import ParamBackwardFusion
 from ..ops.optim import OptimConfig
 from ..parallel import comm_util
 from ..runtime import bootstrap, checkpoint
@@ -286,13 +288,13 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     ring = LossRing(max(1, config.log_every), 2, device, world)
     last = [float("nan")] * 2
 
-    def _flush():
+    def _flush(wait: bool = True):
         nonlocal last
-        # ring.flush() syncs with the host anyway: check the sticky xGMI timeout word
-        # here too, so a timed-out exchange stops the run at the next log point instead
-        # of training on partial sums until the end
+        # check the sticky xGMI timeout word at every log point (one host read, with
+        # several ranks only), so a timed-out exchange stops the run there instead of
+        # training on partial sums until the end
         ddp.check_comm()
-        for step, (vx, vy) in ring.flush():
+        for step, (vx, vy) in ring.flush(wait):
             if rank == 0:
                 logger.log({"loss/lossX": vx}, step=step, commit=False)
                 logger.log({"loss/lossY": vy}, step=step)
@@ -306,30 +308,45 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     # is skipped (reset whenever a capture is abandoned: its zeroing never ran)
     grads_clean = [False]
     xb = {}
+    fuse_opt = world == 1 and os.environ.get("DTP_MODULE_FUSE_OPT", "1") != "0"
+    seed = _Seeds(device)
+    loss_log = os.environ.get("DTP_MODULE_LOSSLOG", "1") != "0"  # A/B: the separate ring put
+    sync_flush = os.environ.get("DTP_MODULE_SYNC_FLUSH", "0") == "1"  # A/B: the blocking flush
 
     def step_body(size):
-        idx_t = idx_static[:size]
         with timer.phase("data"):
             if size not in xb:
                 xb[size] = (torch.empty(size, X.shape[1], device=device), torch.empty(size, Y.shape[1], device=device))
             x, y = xb[size]
-            gather_rows2(X, Y, idx_t, x, y)  # both tensors in one launch
+            if epoch_ring is not None:  # indices from the device epoch ring, cursor advanced on the device
+                gather_rows2_ring(X, Y, epoch_ring, geom.batch, geom.steps_per_epoch, x, y)
+            else:
+                gather_rows2(X, Y, idx_static[:size], x, y)  # both tensors in one launch
             if config.loss == "ce":
                 y = y.view(-1).long()
         if not grads_clean[0]:
             bank.zero_grad()
+        logged = False
         with timer.phase("forward"):
             ox, oy = ddp(x)  # both models' forwards in one launch (ModelBank.forward)
             if isinstance(lossf, MSELoss):
-                lx, ly, lsum = lossf.pair(ox, oy, y)  # both losses and their sum in one launch
+                # both losses, their sum and the loss-log row in one launch
+                lx, ly, lsum = lossf.pair(ox, oy, y, log=ring.device_log() if loss_log else None)
+                logged = loss_log
             else:
                 lx, ly = lossf(ox, y), lossf(oy, y)
                 lsum = lx + ly
-        with timer.phase("backward+allreduce"):
-            lsum.backward()  # independent models: one backward, one bucketed all-reduce
-        with timer.phase("optimizer"):
-            grads_clean[0] = opt.step(zero_grad=True)
-        ring.put_device(lx, ly)
+        # one rank: both models' stage backwards and the flat Adam over both as ONE launch
+        # (ParamBackwardFusion; nothing reads the gradient in between without an all-reduce)
+        with (ParamBackwardFusion() if fuse_opt else contextlib.nullcontext()) as fus:
+            with timer.phase("backward+allreduce"):
+                # independent models: one backward, one bucketed all-reduce; the seed from a
+                # cached tensor of ones (autograd's own is a fill launch per step)
+                lsum.backward(seed.get(lsum.shape) if device.type == "cuda" else None)
+            with timer.phase("optimizer"):
+                grads_clean[0] = opt.step(zero_grad=True, fused=fus.take() if fus is not None else None)
+        if not logged:
+            ring.put_device(lx, ly)
 
     def _abort():
         grads_clean[0] = False
@@ -340,15 +357,28 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     # not gloo-staged buckets (host-driven)
     graphable = device.type == "cuda" and config.launch != "eager" and not trace_enabled() and ddp.graph_safe()
     stepper = CapturedStep(step_body, device, enabled=graphable, on_abort=_abort)
+    # the device epoch ring {cursor, the epoch's indices} of the replayed step's gather: one
+    # fill per epoch instead of an index copy per step (DTP_MODULE_RING=0: the copies, A/B)
+    epoch_ring, ring_epoch = None, None
+    if (graphable and indexer.can_fill_epoch() and ring_gather_ok(X, Y, geom.batch)
+            and os.environ.get("DTP_MODULE_RING", "1") != "0"):
+        epoch_ring = torch.zeros(1 + geom.steps_per_epoch * geom.batch, dtype=torch.int64, device=device)
+        epoch_ring[0] = geom.batch_pos(start)[1] // geom.batch  # the cursor: the first step's batch in its epoch
     for it in range(start, config.iters):
         faults.check(it)
         size = geom.batch_size_at(it)
-        idx_static[:size].copy_(indexer(it))
+        if epoch_ring is not None:
+            ep = geom.batch_pos(it)[0]
+            if ep != ring_epoch:  # stream-ordered after the last replay that read the old epoch
+                indexer.epoch_into(ep, epoch_ring[1:1 + geom.num_samples])
+                ring_epoch = ep
+        else:
+            idx_static[:size].copy_(indexer(it))
         stepper.run(size)
         ring.mark(it)
         if ring.full():
             with timer.phase("loss_reduce"):
-                _flush()
+                _flush(wait=sync_flush)  # no device sync: the rows are logged when they arrive
         if pbar is not None:
             pbar.update(1)
         if config.checkpoint_dir and config.checkpoint_every and (it + 1) % config.checkpoint_every == 0:
@@ -372,6 +402,20 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
             "samples_per_s": geom.batch * (config.iters - start) * world / max(dt, 1e-9), "engine": "module",
             "graph_replays": stepper.replays,
             **({"phases": timer.summary()} if trace_enabled() else {})}
+
+
+class _Seeds:
+    """d loss / d loss: one cached tensor of ones per shape (a captured step replays it)."""
+
+    def __init__(self, device):
+        self.device = device
+        self._t: dict = {}
+
+    def get(self, shape):
+        t = self._t.get(tuple(shape))
+        if t is None:
+            t = self._t[tuple(shape)] = torch.ones(shape, dtype=torch.float32, device=self.device)
+        return t
 
 
 # ----------------------------------------------------------------------------- stock engine

@@ -58,12 +58,15 @@ class _FusedMSEPair(torch.autograd.Function):
     """(mse(a1, b), mse(a2, b), their sum) in one launch; backward in one launch."""
 
     @staticmethod
-    def forward(ctx, a1, a2, b):
+    def forward(ctx, a1, a2, b, log):
         ctx.set_materialize_grads(False)  # unused outputs' gradients stay None (no zero fills)
         a1_, a2_, b_ = a1.contiguous(), a2.contiguous(), b.contiguous()
         o1, o2, osum = (torch.empty((), dtype=torch.float32, device=a1.device) for _ in range(3))
+        ring, slot = log if log is not None else (None, None)
         nat.check(nat.load().dtp_mse_pair_fwd(nat.ptr(a1_), nat.ptr(a2_), nat.ptr(b_), b_.numel(), nat.ptr(o1),
-                                              nat.ptr(o2), nat.ptr(osum), nat.stream_ptr()), "dtp_mse_pair_fwd")
+                                              nat.ptr(o2), nat.ptr(osum), nat.ptr(ring), nat.ptr(slot),
+                                              0 if ring is None else ring.shape[1], nat.stream_ptr()),
+                  "dtp_mse_pair_fwd")
         ctx.save_for_backward(a1_, a2_, b_)
         ctx.shape = b.shape
         return o1, o2, osum
@@ -71,9 +74,9 @@ class _FusedMSEPair(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g1, g2, gsum):
         a1_, a2_, b_ = ctx.saved_tensors
-        n1, n2, nb = ctx.needs_input_grad
+        n1, n2, nb, _ = ctx.needs_input_grad
         if (g1 is None and g2 is None and gsum is None) or not (n1 or n2 or nb):
-            return None, None, None
+            return None, None, None, None
         ga1 = torch.empty_like(a1_) if n1 else None
         ga2 = torch.empty_like(a2_) if n2 else None
         gb = torch.empty_like(b_) if nb else None
@@ -83,18 +86,28 @@ class _FusedMSEPair(torch.autograd.Function):
                                               nat.ptr(gs_), b_.numel(), nat.ptr(ga1), nat.ptr(ga2), nat.ptr(gb),
                                               nat.stream_ptr()), "dtp_mse_pair_bwd")
         view = lambda t: None if t is None else t.view(ctx.shape)  # noqa: E731
-        return view(ga1), view(ga2), view(gb)
+        return view(ga1), view(ga2), view(gb), None
 
 
-def mse_loss_pair(input1: torch.Tensor, input2: torch.Tensor, target: torch.Tensor):
+def mse_loss_pair(input1: torch.Tensor, input2: torch.Tensor, target: torch.Tensor, log=None):
     """(mse(input1, target), mse(input2, target), their sum): the reference's two models'
     losses on one batch (``loss_X + loss_Y``) in ONE launch forward and one backward on
     the GPU (the unfused form is 2 forward launches, an add and 2 backward launches);
-    torch's ops elsewhere.  The same values, bit for bit, as the separate calls."""
-    if _fused_ok(input1, target) and _fused_ok(input2, target):
-        return _FusedMSEPair.apply(input1, input2, target)
+    torch's ops elsewhere.  The same values, bit for bit, as the separate calls.
+
+    ``log``: a device loss log ``(rows [cap, >= 2] fp32, slot [1] int64)`` -- the
+    engine's ``LossRing`` -- into whose row ``slot`` the two losses are also written (slot
+    advanced) by the same launch; the caller keeps the slot within ``cap``."""
+    if _fused_ok(input1, target) and _fused_ok(input2, target) and (
+            log is None or (log[0].is_cuda and log[0].dtype == torch.float32 and log[0].dim() == 2
+                            and log[0].shape[1] >= 2 and log[0].is_contiguous() and log[1].dtype == torch.int64)):
+        return _FusedMSEPair.apply(input1, input2, target, log)
     l1 = nn.functional.mse_loss(input1, target)
     l2 = nn.functional.mse_loss(input2, target)
+    if log is not None:
+        rows, slot = log
+        rows[:, :2].index_copy_(0, slot, torch.stack([l1.detach(), l2.detach()]).view(1, 2).to(rows.dtype))
+        slot.add_(1)
     return l1, l2, l1 + l2
 
 
@@ -115,10 +128,12 @@ class MSELoss(nn.Module):
     def forward(self, input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         return mse_loss(input, target, self.reduction)
 
-    def pair(self, input1: torch.Tensor, input2: torch.Tensor, target: torch.Tensor):
+    def pair(self, input1: torch.Tensor, input2: torch.Tensor, target: torch.Tensor, log=None):
         """Two predictions against one target: (loss1, loss2, loss1 + loss2) in one fused
-        launch (``mse_loss_pair``; reduction="mean" only)."""
+        launch (``mse_loss_pair``; reduction="mean" only; ``log``: see there)."""
         if self.reduction != "mean":
+            if log is not None:
+                raise ValueError("MSELoss.pair(log=...) needs reduction='mean'")
             l1, l2 = self(input1, target), self(input2, target)
             return l1, l2, l1 + l2
-        return mse_loss_pair(input1, input2, target)
+        return mse_loss_pair(input1, input2, target, log)

@@ -142,21 +142,23 @@ def stage_forward(x: torch.Tensor, flat: torch.Tensor, spec: MlpSpec, save: bool
 
 
 class ParamBackwardFusion:
-    """A window in which a whole-model stage backward that adds into a persistent flat
-    gradient span (and wants no input gradient) is not launched at once but handed to the
-    next flat optimizer step over exactly that span, which runs both as ONE launch
-    (``csrc/mlp_stage.hip:mlp_stage_bwd_opt_kernel``; ``FlatOptimizer.step(fused=...)``).
+    """A window in which whole-model stage backwards that add into persistent flat
+    gradient spans (and want no input gradient) are not launched at once but handed to the
+    next flat optimizer step over exactly those spans, which runs them and itself as ONE
+    launch (``csrc/mlp_stage.hip:mlp_stage_bwd_opt_kernel``, one block per model;
+    ``FlatOptimizer.step(fused=...)``): the Trainer's toggled model (its backward + its
+    optimizer: 2 launches -> 1), the module engine's ModelBank (both backwards + the one
+    flat Adam over both models: 3 -> 1).
 
-    The Trainer's module path opens it around ``loss.backward()`` + the optimizer step
-    at one rank (``Trainer._optimizer_steps``): there nothing reads the gradient in
-    between (no all-reduce), and the toggled model's stage backward is the backward's
-    last launch.  Whatever is still pending when the window closes normally -- a second
-    stage, an optimizer over another span -- is launched as it was; an exception drops it
-    (that backward's gradient is abandoned anyway).  Reference: PL 1.5's per-optimizer
-    backward + step, ``/root/reference/demo_pytorch_lightning.py:27-40``."""
+    Opened around ``loss.backward()`` + the optimizer step at one rank: there nothing
+    reads the gradient in between (no all-reduce).  Whatever is still pending when the
+    window closes normally -- an optimizer over other spans, none at all -- is launched
+    as it was; an exception drops it (that backward's gradient is abandoned anyway).
+    Reference: PL 1.5's per-optimizer backward + step,
+    ``/root/reference/demo_pytorch_lightning.py:27-40``; ``demo.py:105-111``."""
 
     def __init__(self):
-        self.pending = None
+        self.pending: list = []
         self._prev = None
 
     def __enter__(self):
@@ -167,19 +169,21 @@ class ParamBackwardFusion:
     def __exit__(self, et, ev, tb):
         global _FUSION
         _FUSION = self._prev
-        p, self.pending = self.pending, None
-        if p is not None and et is None:
-            p.launch()
+        p, self.pending = self.pending, []
+        if p and et is None:
+            _launch_pending(p)
         return False
 
     def defer(self, pend) -> None:
-        if self.pending is not None:
-            self.pending.launch()
-        self.pending = pend
+        if self.pending and (len(self.pending) >= nat.STAGE_MULTI_MAX or not self.pending[0].compatible(pend)):
+            _launch_pending(self.pending)
+            self.pending = []
+        self.pending.append(pend)
 
     def take(self):
-        p, self.pending = self.pending, None
-        return p
+        """The deferred backwards (model order), or None; the caller launches them."""
+        p, self.pending = self.pending, []
+        return p or None
 
 
 _FUSION: ParamBackwardFusion | None = None  # read from autograd's device thread too
@@ -193,20 +197,43 @@ class _PendingStageBackward:
     def __init__(self, args, key, keep, device):
         self.args, self.key, self.keep, self.device = args, key, keep, device
 
-    def matches(self, params: torch.Tensor, grad: torch.Tensor) -> bool:
-        """Whether a one-row optimizer over (params, grad) is exactly this stage's span."""
-        P = self.keep[1].numel()
-        return (params.numel() == P and grad.numel() >= P and params.data_ptr() == self.args.params
-                and grad.data_ptr() == self.args.grad_params)
+    def compatible(self, other) -> bool:
+        return other.key == self.key and other.device == self.device
 
     def launch(self) -> None:
         nat.check(nat.require(self.device).dtp_mlp_stage_bwd(ctypes.byref(self.args), *self.key, nat.stream_ptr()),
                   "dtp_mlp_stage_bwd")
 
-    def launch_with_optimizer(self, opt_args) -> None:
-        nat.check(nat.require(self.device).dtp_mlp_stage_bwd_opt(ctypes.byref(self.args), ctypes.byref(opt_args),
-                                                                 *self.key, nat.stream_ptr()),
-                  "dtp_mlp_stage_bwd_opt")
+
+def _launch_pending(pends) -> None:
+    for p in pends:
+        p.launch()
+
+
+def fused_rows_match(pends, params: torch.Tensor, grad: torch.Tensor) -> bool:
+    """Whether an optimizer over [n, P] (params, grad) rows is exactly these deferred stage
+    backwards, row i = stage i."""
+    if not pends or params.dim() != 2 or grad.dim() != 2 or params.shape[0] != len(pends) \
+            or grad.shape != params.shape or not grad.is_contiguous() or not params.is_contiguous():
+        return False
+    P = params.shape[1]
+    for i, p in enumerate(pends):
+        if (p.keep[1].numel() != P or p.args.params != params[i].data_ptr()
+                or p.args.grad_params != grad[i].data_ptr() or not p.compatible(pends[0])):
+            return False
+    return True
+
+
+def launch_fused_with_optimizer(pends, opt_args) -> None:
+    """The deferred stage backwards and the optimizer step (``opt_args``, one row per
+    stage) as ONE launch."""
+    m = nat.StageMulti()
+    m.n = len(pends)
+    for i, p in enumerate(pends):
+        m.stage[i] = p.args
+    nat.check(nat.require(pends[0].device).dtp_mlp_stage_bwd_opt(ctypes.byref(m), ctypes.byref(opt_args),
+                                                                 *pends[0].key, nat.stream_ptr()),
+              "dtp_mlp_stage_bwd_opt")
 
 
 def stage_backward(x, flat, spec: MlpSpec, out, saved, grad_out, need_grad_in: bool = True,

@@ -119,7 +119,7 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
     to bf16 in the same pass, row i at ``shadow[i, :P]``.  ``zero_grad``: the gradient
     rows are zeroed in the same pass once read (the loss slots are not).  ``fused``: a
     deferred stage backward (``ops.mlp.ParamBackwardFusion``) whose span is exactly this
-    one-row optimizer's: the backward and this step run as one launch.
+    optimizer's rows (row i = stage i): the backwards and this step run as one launch.
     """
     n_models, P = params.shape
     if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.dim() != 2 or shadow.shape[0] != n_models
@@ -131,13 +131,16 @@ def flat_optimizer_step(params, m, v, step, grad, cfg: OptimConfig, grad_scale: 
                         nat.ptr(loss_log), 0 if loss_log is None else loss_log.shape[0], n_models, P, cfg.kind,
                         loss_scale, 1 if zero_grad else 0, cfg.hyper(slope, grad_scale), nat.ptr(shadow),
                         0 if shadow is None else shadow.stride(0))
-        if fused is not None:  # the stage backward that produced `grad`, in the same launch
-            fused.launch_with_optimizer(a)
+        if fused is not None:  # the stage backwards that produced `grad`, in the same launch
+            from .mlp import launch_fused_with_optimizer
+
+            launch_fused_with_optimizer(fused, a)
             return
         nat.check(lib.dtp_flat_optimizer(ctypes.byref(a), nat.stream_ptr()), "dtp_flat_optimizer")
         return
     if fused is not None:
-        fused.launch()
+        for p in fused:
+            p.launch()
     g = grad[: n_models * P].view(n_models, P) * grad_scale
     for i in range(n_models):
         t = int(step[i])
@@ -179,19 +182,22 @@ class FlatOptimizer:
     @torch.no_grad()
     def step(self, zero_grad: bool = False, fused=None) -> bool:
         """One step; ``zero_grad``: zero the gradient in the same launch (no separate fill
-        before the next backward).  ``fused``: a deferred stage backward
-        (``ops.mlp.ParamBackwardFusion.take()``): run in the same launch when its span is
-        exactly this optimizer's one row, else launched first.  Returns whether the
+        before the next backward).  ``fused``: deferred stage backwards
+        (``ops.mlp.ParamBackwardFusion.take()``): run in the same launch when their spans
+        are exactly this optimizer's rows, else launched first.  Returns whether the
         gradient was zeroed (not when it had to be staged through a copy)."""
         # the kernel reads grad[i*P : (i+1)*P] only (the loss slots behind them are
         # read only with a loss log), so a contiguous [n, P] gradient is used in place
         n, P = self.params.shape
         sh = self.shadow
         fresh = sh is not None and sh._token == sh._current()  # else the next forward re-casts anyway
-        if fused is not None and not (n == 1 and not fresh and self.grad.is_contiguous()
-                                      and fused.matches(self.params, self.grad)):
-            fused.launch()
-            fused = None
+        if fused is not None:
+            from .mlp import fused_rows_match
+
+            if fresh or not fused_rows_match(fused, self.params, self.grad):
+                for p in fused:
+                    p.launch()
+                fused = None
         if self.grad.is_contiguous() and self.grad.device == self.params.device:
             buf = self.grad.view(-1)
         else:

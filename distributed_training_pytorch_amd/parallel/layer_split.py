@@ -474,8 +474,12 @@ class FusedLayerSplit:
                 a.cache_data = 1
                 a.dp_world, a.dp_rank = self.world, self.rank
                 a.optim = nat.MODE_ADAM if self.optim.name == "adam" else nat.MODE_SGD
+                # bit 2: both ends of this stage's on-GPU links run in this launch, so their
+                # members may switch to plain stores after the XCC hello (split_lanes.hip);
+                # separate per-stage launches keep write-through links (measured faster there)
+                same = all((s2 in stages) for s2 in (s - 1, s + 1) if 0 <= s2 < K)
                 a.link_local = (int(s > 0 and self.link_local[s - 1])
-                                | (int(s + 1 < K and self.link_local[s]) << 1))
+                                | (int(s + 1 < K and self.link_local[s]) << 1) | (int(same) << 2))
                 a.smp = geom.to_native()
                 if dev in self.rings and (s == 0 or s == K - 1):
                     self.rings[dev].native(a.smp)

@@ -121,6 +121,7 @@ class LossRing:
         self.world = world
         self.group = group
         self.steps: list[int] = []
+        self._inflight: list = []  # (event, pinned rows, steps) queued by flush(wait=False)
 
     def put_device(self, *values) -> None:
         """Device half of ``put`` (graph-capturable): row[slot] = values; slot += 1."""
@@ -129,6 +130,11 @@ class LossRing:
         row = torch.stack([v.detach().reshape(()).float() for v in values]).view(1, -1)
         self.buf.index_copy_(0, self.slot, row)
         self.slot.add_(1)
+
+    def device_log(self):
+        """``(rows, slot)`` for a kernel that writes the row itself (``MSELoss.pair(log=)``:
+        the losses and the ring put in the loss's own launch instead of 3 more)."""
+        return self.buf, self.slot
 
     def mark(self, step: int) -> None:
         """Host half of ``put``: the row just written holds ``step``."""
@@ -141,16 +147,38 @@ class LossRing:
     def full(self) -> bool:
         return len(self.steps) == self.buf.shape[0]
 
-    def flush(self) -> list[tuple[int, list[float]]]:
-        if not self.steps:
-            return []
-        from ..parallel import comm_util
+    def flush(self, wait: bool = True) -> list[tuple[int, list[float]]]:
+        """Reduce the chunk and return the (step, values) rows that are on the host.
+        ``wait=False`` (periodic flushes inside a run): the chunk's copy to pinned memory is
+        only queued -- behind it the next steps' device work keeps the GPU busy -- and its
+        rows come back from a later flush once the copy has arrived; ``wait=True``: every
+        chunk, now.  Rows always come back in step order."""
+        import torch
 
-        k = len(self.steps)
-        chunk = self.buf[:k]
-        comm_util.all_reduce_(chunk, self.group)
-        vals = (chunk / self.world).cpu().tolist()
-        out = list(zip(self.steps, vals))
-        self.steps = []
-        self.slot.zero_()
+        if self.steps:
+            from ..parallel import comm_util
+
+            k = len(self.steps)
+            chunk = self.buf[:k]
+            comm_util.all_reduce_(chunk, self.group)
+            ev = None
+            if chunk.is_cuda:
+                host = torch.empty(chunk.shape, dtype=chunk.dtype, pin_memory=True)
+                host.copy_(chunk, non_blocking=True)  # stream-ordered before the rows are reused
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host = chunk.clone()
+            self._inflight.append((ev, host, self.steps))
+            self.steps = []
+            self.slot.zero_()
+        out = []
+        while self._inflight and (wait or self._inflight[0][0] is None or self._inflight[0][0].query()):
+            ev, host, steps = self._inflight.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            vals = host.tolist()
+            if self.world > 1:
+                vals = [[v / self.world for v in row] for row in vals]
+            out.extend(zip(steps, vals))
         return out

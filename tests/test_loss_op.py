@@ -214,3 +214,42 @@ def test_trainer_epoch_ring_gather_on_device(shuffle):
         rows = torch.tensor(ref[b * 128:(b + 1) * 128], device="cuda")
         assert torch.equal(out[0], X[rows]) and torch.equal(out[1], Y[rows]), k
     assert int(loader.ring[0]) == 9
+
+
+@pytest.mark.gpu
+def test_mse_loss_pair_writes_the_loss_log_row_in_its_launch():
+    """``mse_loss_pair(log=(rows, slot))``: the two losses also land in row ``slot`` of the
+    engine's device loss log and the slot advances -- in the loss's own launch, replayed
+    by a captured graph row after row."""
+    from distributed_training_pytorch_amd.ops.loss import mse_loss_pair
+
+    torch.manual_seed(4)
+    rows = torch.full((5, 2), -1.0, device="cuda")
+    slot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    a1, a2, b = (torch.randn(64, 1, device="cuda") for _ in range(3))
+    l1, l2, _ = mse_loss_pair(a1, a2, b, log=(rows, slot))
+    torch.cuda.synchronize()
+    assert int(slot) == 1 and rows[0, 0] == l1 and rows[0, 1] == l2 and (rows[1:] == -1).all()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=s):
+        o1, o2, _ = mse_loss_pair(a1, a2, b, log=(rows, slot))
+    for k in range(1, 4):
+        a1.add_(0.5)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(slot) == k + 1
+        assert rows[k, 0] == o1 and rows[k, 1] == o2
+        torch.testing.assert_close(o1, torch.nn.functional.mse_loss(a1, b), rtol=1e-5, atol=1e-7)
+    assert (rows[4] == -1).all()
+
+
+def test_mse_loss_pair_log_cpu_form():
+    from distributed_training_pytorch_amd.ops.loss import mse_loss_pair
+
+    rows = torch.zeros(3, 2)
+    slot = torch.ones(1, dtype=torch.int64)
+    a1, a2, b = torch.randn(8, 1), torch.randn(8, 1), torch.randn(8, 1)
+    l1, l2, _ = mse_loss_pair(a1, a2, b, log=(rows, slot))
+    assert int(slot) == 2 and rows[1, 0] == l1 and rows[1, 1] == l2 and not rows[0].any() and not rows[2].any()

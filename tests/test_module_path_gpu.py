@@ -133,3 +133,69 @@ def test_trainer_graph_copies_log_every_step_like_eager(tmp_path):
     assert c4 == c1 == ce
     for k in s1:
         assert torch.equal(s4[k], s1[k]) and torch.equal(s1[k], se[k]), k
+
+
+def _train_bank(fuse: bool, steps: int = 6, batch: int = 256):
+    import contextlib
+
+    from distributed_training_pytorch_amd.models.bank import ModelBank
+    from distributed_training_pytorch_amd.ops.loss import MSELoss
+    from distributed_training_pytorch_amd.ops.mlp import ParamBackwardFusion
+    from distributed_training_pytorch_amd.ops.optim import FlatOptimizer, OptimConfig
+    from distributed_training_pytorch_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(7)
+    bank = ModelBank(2).cuda()
+    ddp = FlatDDP(bank, flat_params=bank.flat, flat_grad=bank.flat_grad)
+    opt = FlatOptimizer(bank.flat, bank.flat_grad, OptimConfig(name="adam", lr=1e-2))
+    lossf = MSELoss()
+    g = torch.Generator(device="cuda").manual_seed(2)
+    taken = []
+    for _ in range(steps):
+        x = torch.randn(batch, 2, device="cuda", generator=g)
+        y = torch.randn(batch, 1, device="cuda", generator=g)
+        bank.zero_grad()
+        with (ParamBackwardFusion() if fuse else contextlib.nullcontext()) as fus:
+            ox, oy = ddp(x)
+            _, _, lsum = lossf.pair(ox, oy, y)
+            lsum.backward()
+            pend = fus.take() if fus is not None else None
+            taken.append(0 if pend is None else len(pend))
+            opt.step(zero_grad=True, fused=pend)
+    torch.cuda.synchronize()
+    return [t.detach().clone() for t in (bank.flat, opt.m, opt.v, opt.step_ctr, bank.flat_grad)], taken
+
+
+@pytest.mark.gpu
+def test_bank_backwards_fused_with_the_two_model_optimizer_is_bitwise():
+    """The module engine's ModelBank under ParamBackwardFusion: both models' stage
+    backwards and the one flat Adam over both rows as ONE launch (one block per model),
+    bitwise the three separate launches."""
+    from distributed_training_pytorch_amd import _native as nat
+
+    nat.require(torch.device("cuda", 0))
+    ref, t0 = _train_bank(False)
+    got, t1 = _train_bank(True)
+    assert t0 == [0] * 6 and t1 == [2] * 6
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    assert not got[4].any()
+
+
+@pytest.mark.gpu
+def test_loss_ring_flush_without_sync_returns_every_row_in_order():
+    """LossRing.flush(wait=False): the chunk's copy is queued, its rows come back from a
+    later flush (or the final wait=True one) -- every row once, in step order, with the
+    values the device wrote."""
+    from distributed_training_pytorch_amd.utils.logging import LossRing
+
+    ring = LossRing(4, 2, torch.device("cuda", 0))
+    got = []
+    for step in range(10):
+        v = torch.tensor([float(step), -float(step)], device="cuda")
+        ring.put(step, v[0], v[1])
+        if ring.full():
+            got += ring.flush(wait=False)
+    got += ring.flush(wait=True)
+    assert [s for s, _ in got] == list(range(10))
+    assert all(vals == [float(s), -float(s)] for s, vals in got)
