@@ -199,3 +199,42 @@ def test_loss_ring_flush_without_sync_returns_every_row_in_order():
     got += ring.flush(wait=True)
     assert [s for s, _ in got] == list(range(10))
     assert all(vals == [float(s), -float(s)] for s, vals in got)
+
+
+def test_param_backward_fusion_window_cpu():
+    """The deferral window's bookkeeping (no GPU): backwards queue in model order, a
+    different shape or device flushes what waits, leftovers launch when the window closes,
+    an exception drops them, and windows nest."""
+    from distributed_training_pytorch_amd.ops import mlp
+
+    launched = []
+
+    class Fake:
+        def __init__(self, name, key=(2, 10, 5, 1, 0), device="cuda:0"):
+            self.name, self.key, self.device = name, key, device
+
+        def compatible(self, other):
+            return other.key == self.key and other.device == self.device
+
+        def launch(self):
+            launched.append(self.name)
+
+    with mlp.ParamBackwardFusion() as f:
+        assert mlp._FUSION is f
+        f.defer(Fake("a"))
+        f.defer(Fake("b"))
+        assert [p.name for p in f.take()] == ["a", "b"] and f.take() is None
+        f.defer(Fake("c"))
+        f.defer(Fake("d", key=(2, 15, 5, 1, 0)))  # another shape: "c" goes out first
+        assert launched == ["c"]
+        with mlp.ParamBackwardFusion() as inner:
+            assert mlp._FUSION is inner
+        assert mlp._FUSION is f
+    assert mlp._FUSION is None and launched == ["c", "d"]  # the leftover launched at exit
+    try:
+        with mlp.ParamBackwardFusion() as f:
+            f.defer(Fake("e"))
+            raise RuntimeError("backward failed")
+    except RuntimeError:
+        pass
+    assert launched == ["c", "d"] and mlp._FUSION is None  # dropped
