@@ -869,6 +869,7 @@ extern "C" int dtp_gemm(const DtpGemmArgs* in, void* stream) {
     switch (a.fast - 2) {
       case 32: return gemm::launch_ph8(a, s, 0);  // 8-phase, balanced reads (gemm_ph8.hip)
       case 34: return gemm::launch_ph8(a, s, 2);  // 8-phase, reads 12/4/8/0 per phase
+      case 35: return gemm::launch_ph8(a, s, 3);  // 8-phase balanced, persistent tile walk
       default: return gemm::launch_fast(a, s);    // two-buffer LDS-DMA kernel
     }
   }

@@ -39,11 +39,12 @@ DTP_DEV float load_elem(const char* p) {
 struct TileId {
   int m0, n0, ks;
 };
+// (b, nb): the tile id and the id count -- a workgroup's blockIdx.x / gridDim.x, or a
+// persistent workgroup's current tile of all tiles (its XCD is b & 7 whenever the grid
+// is a multiple of 8, so its tiles stay in its XCD's range)
 template <int BMT, int BNT>
-DTP_DEV TileId decode_tile(const DtpGemmArgs& a) {
+DTP_DEV TileId decode_tile_at(const DtpGemmArgs& a, int b, int nb) {
   const int tm = (a.M + BMT - 1) / BMT, tn = (a.N + BNT - 1) / BNT;
-  int b = blockIdx.x;
-  const int nb = gridDim.x;
   if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
   TileId id;
   id.ks = b % a.splitk;
@@ -53,6 +54,10 @@ DTP_DEV TileId decode_tile(const DtpGemmArgs& a) {
   id.m0 = (first_m + (t % (8 * tn)) % gsz) * BMT;
   id.n0 = ((t % (8 * tn)) / gsz) * BNT;
   return id;
+}
+template <int BMT, int BNT>
+DTP_DEV TileId decode_tile(const DtpGemmArgs& a) {
+  return decode_tile_at<BMT, BNT>(a, blockIdx.x, gridDim.x);
 }
 
 
@@ -104,9 +109,14 @@ DTP_DEV void bf16x8_to_f32(const uint4& g, float (&x)[8]) {
 // one pass = fragment rows 4H .. 4H+3 (H a template parameter: acc is indexed
 // statically, so it stays in registers)
 // (J0: first of the 4 fragment columns staged, for waves holding more than 4)
-template <int H, int J0 = 0, int NJ = 4>
+// ROWS (64 or 16): rows staged per pass -- 16 = one fragment row (II0) of the row half,
+// a quarter of the LDS staging (the persistent GEMM stages while the next tile's operands
+// stream into the rest of LDS); row0 is then the fragment row's first row
+template <int H, int J0 = 0, int NJ = 4, int ROWS = 64, int II0 = 0>
 DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ], float* buf, const float (&bias)[8],
                                 int row0, int ncol, bool vec, int lane) {
+  static_assert(ROWS == 64 || ROWS == 16, "64- or 16-row passes");
+  constexpr int NII = ROWS / 16, NU = ROWS / 8 < 4 ? ROWS / 8 : 4;
   const int lr = lane & 15, lg = lane >> 4, c8 = lane & 7, rl = lane >> 3;
   char* C = static_cast<char*>(a.C);
   const uint16_t* aux = static_cast<const uint16_t*>(a.aux);
@@ -114,18 +124,19 @@ DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ],
   constexpr int h = H;
   {
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
+    for (int ii = 0; ii < NII; ++ii)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) buf[(16 * ii + 4 * lg + r) * kEpiStride + 16 * j + lr] = acc[4 * h + ii][J0 + j][r];
+        for (int r = 0; r < 4; ++r)
+          buf[(16 * ii + 4 * lg + r) * kEpiStride + 16 * j + lr] = acc[4 * h + II0 + ii][J0 + j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's stores land before its own reads (LDS is in order per wave)
 #pragma unroll
-    for (int t0 = 0; t0 < 8; t0 += 4) {
-      float v[4][8];
-      int mrow[4];
+    for (int t0 = 0; t0 < ROWS / 8; t0 += NU) {
+      float v[NU][8];
+      int mrow[NU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < NU; ++u) {
         const int lrow = rl + 8 * (t0 + u);
         mrow[u] = row0 + lrow;
         const float4 x0 = *reinterpret_cast<const float4*>(buf + lrow * kEpiStride + 8 * c8);
@@ -136,9 +147,9 @@ DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ],
       }
       if (vec) {
         // every operand of the 4 rows requested before any is used (rows past M clamped, never stored)
-        uint4 g[4], oc[4][2];
+        uint4 g[NU], oc[NU][2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
           const long long mr = min(mrow[u], a.M - 1);
           if (aux) g[u] = *reinterpret_cast<const uint4*>(aux + mr * a.ldaux + ncol);
           if (a.accumulate) {
@@ -151,7 +162,7 @@ DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ],
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
           float y[8];
 #pragma unroll
           for (int c = 0; c < 8; ++c) y[c] = a.alpha * v[u][c] + bias[c];
@@ -191,7 +202,7 @@ DTP_DEV void fast_epilogue_pass(const DtpGemmArgs& a, const f32x4 (&acc)[8][NJ],
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
           if (mrow[u] >= a.M) continue;
 #pragma unroll
           for (int c = 0; c < 8; ++c)

@@ -141,22 +141,39 @@ DTP_DEV void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool TA, bool TB, bool BAL, bool SPLIT>
+// PERSIST: one workgroup per CU walks the tiles t = blockIdx.x + i * gridDim.x; after a
+// tile's K loop it issues the NEXT tile's five prologue parts (buffer 0 and part 3 of
+// buffer 1) before its own epilogue, which stages 16-row passes in the LDS gap between
+// them ([64 KiB, 98 KiB)), so the next tile's operand fill runs under this tile's
+// write-back instead of after a new workgroup's start (profiles/r4_gemm: ~3 points of
+// per-tile cost).  Balanced schedule only (its prologue leaves that gap free).
+template <bool TA, bool TB, bool BAL, bool SPLIT, bool PERSIST = false>
 __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
+  static_assert(!PERSIST || (BAL && !SPLIT), "the persistent walk runs the balanced, unsplit schedule");
   __shared__ __align__(16) char lds[kLds];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  const TileId id = decode_tile<256, 256>(a);
-  const int m0 = id.m0, n0 = id.n0, nk = a.K / 64 / a.splitk;  // K-tiles of this block's K-slice
+  const int ntiles = PERSIST ? ((a.M + 255) / 256) * ((a.N + 255) / 256) : 0;
+  int tcur = blockIdx.x;
+  if (PERSIST && tcur >= ntiles) return;  // the grid is rounded up to a multiple of 8 (whole workgroup)
+  TileId id = PERSIST ? decode_tile_at<256, 256>(a, tcur, ntiles) : decode_tile<256, 256>(a);
+  int m0 = id.m0, n0 = id.n0;
+  const int nk = a.K / 64 / a.splitk;  // K-tiles of this block's K-slice
 
   uint32_t oSA[2][2], oSB[2][2];
-  part_sources<TA>(oSA, a.lda, m0, a.M, wave, lane);
-  part_sources<TB>(oSB, a.ldb, n0, a.N, wave, lane);
   const uint32_t kbA = TA ? static_cast<uint32_t>(128 * a.lda) : 128u, kbB = TB ? static_cast<uint32_t>(128 * a.ldb) : 128u;
-  // uniform operand bases at the block's first row / column and first K-tile
-  const uint32_t kt0 = static_cast<uint32_t>(id.ks * nk);
-  const char* gA = static_cast<const char*>(a.A) + (TA ? m0 : m0 * a.lda) * 2 + kt0 * kbA;
-  const char* gB = static_cast<const char*>(a.B) + (TB ? n0 : n0 * a.ldb) * 2 + kt0 * kbB;
+  const char* gA;
+  const char* gB;
+  // this lane's DMA sources and the uniform operand bases at the tile's first row /
+  // column and first K-tile
+  auto set_sources = [&]() {
+    part_sources<TA>(oSA, a.lda, m0, a.M, wave, lane);
+    part_sources<TB>(oSB, a.ldb, n0, a.N, wave, lane);
+    const uint32_t kt0 = static_cast<uint32_t>(id.ks * nk);
+    gA = static_cast<const char*>(a.A) + (TA ? m0 : m0 * a.lda) * 2 + kt0 * kbA;
+    gB = static_cast<const char*>(a.B) + (TB ? n0 : n0 * a.ldb) * 2 + kt0 * kbB;
+  };
+  set_sources();
 
   // one part (P: 0 = A0, 1 = A1, 2 = B0, 3 = B1) of K-tile `tile` into its buffer,
   // or into the sink past the last tile (same wait accounting every phase)
@@ -181,10 +198,6 @@ __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
   part_offsets<TB, 2>(oB, wc * 32, lane);
 
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
   auto rdA = [&](const char* part) {
@@ -229,14 +242,22 @@ __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
 
   // prologue: B0, A0, B1, A1 of tile 0 and B0 of tile 1 (the order the loop's
   // phases -5 .. -1 would have staged them); vmcnt(6) retires B0 and A0 of tile 0
-  stage(P2{}, 0);
-  stage(P0{}, 0);
-  stage(P3{}, 0);
-  stage(P1{}, 0);
-  if constexpr (BAL) stage(P3{}, 1);
-  else stage(P2{}, 1);
+  auto prologue = [&]() {
+    stage(P2{}, 0);
+    stage(P0{}, 0);
+    stage(P3{}, 0);
+    stage(P1{}, 0);
+    if constexpr (BAL) stage(P3{}, 1);
+    else stage(P2{}, 1);
+  };
+  prologue();
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   barrier();
+  for (;;) {  // one pass unless PERSIST
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (wave >= 4) barrier();  // stagger: waves 4-7 one barrier behind
 
   if constexpr (BAL) {
@@ -323,19 +344,47 @@ __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   barrier();
 
-  // epilogue: LDS-staged 16-byte rows, one pass per row quadrant; the lane's 8
-  // staged columns 8 (lane & 7) .. +8 sit in column quadrant (lane & 7) >> 2
-  float* ebuf = reinterpret_cast<float*>(lds) + wave * kEpiWaveFloats;
+  // PERSIST: the next tile's prologue parts go out now, under this tile's epilogue
+  const int em0 = m0, en0 = n0;
+  bool next = false;
+  if constexpr (PERSIST) {
+    tcur += gridDim.x;
+    next = tcur < ntiles;
+    if (next) {
+      id = decode_tile_at<256, 256>(a, tcur, ntiles);
+      m0 = id.m0;
+      n0 = id.n0;
+      set_sources();
+      prologue();
+    }
+  }
+
+  // epilogue: LDS-staged 16-byte rows, one pass per row quadrant (PERSIST: per fragment
+  // row, in the LDS the prologue leaves free); the lane's 8 staged columns 8 (lane & 7)
+  // .. +8 sit in column quadrant (lane & 7) >> 2
+  float* ebuf = PERSIST ? reinterpret_cast<float*>(lds + kBuf) + wave * (16 * kEpiStride)
+                        : reinterpret_cast<float*>(lds) + wave * kEpiWaveFloats;
   const int c8 = lane & 7;
-  const int ncol = n0 + (c8 >> 2) * 128 + wc * 32 + 8 * (c8 & 3);
+  const int ncol = en0 + (c8 >> 2) * 128 + wc * 32 + 8 * (c8 & 3);
   auto store = [&](const DtpGemmArgs& e) {
     const uintptr_t cp = reinterpret_cast<uintptr_t>(e.C), ap = reinterpret_cast<uintptr_t>(e.aux);
     const bool vec = ncol + 8 <= e.N && e.ldc % 8 == 0 && (cp & 15) == 0 && (!e.aux || (e.ldaux % 8 == 0 && (ap & 15) == 0));
     float bias[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) bias[c] = (e.bias && ncol + c < e.N) ? e.bias[ncol + c] : 0.f;
-    fast_epilogue_pass<0>(e, acc, ebuf, bias, m0 + wr * 64, ncol, vec, lane);
-    fast_epilogue_pass<1>(e, acc, ebuf, bias, m0 + 128 + wr * 64, ncol, vec, lane);
+    if constexpr (PERSIST) {
+      static_for<0, 4>([&](auto IC) {
+        constexpr int ii = decltype(IC)::value;
+        fast_epilogue_pass<0, 0, 4, 16, ii>(e, acc, ebuf, bias, em0 + wr * 64 + 16 * ii, ncol, vec, lane);
+      });
+      static_for<0, 4>([&](auto IC) {
+        constexpr int ii = decltype(IC)::value;
+        fast_epilogue_pass<1, 0, 4, 16, ii>(e, acc, ebuf, bias, em0 + 128 + wr * 64 + 16 * ii, ncol, vec, lane);
+      });
+    } else {
+      fast_epilogue_pass<0>(e, acc, ebuf, bias, em0 + wr * 64, ncol, vec, lane);
+      fast_epilogue_pass<1>(e, acc, ebuf, bias, em0 + 128 + wr * 64, ncol, vec, lane);
+    }
   };
   if constexpr (SPLIT) {  // raw f32 partial sums of this K-slice: work[ks][M][N]; splitk_reduce_kernel applies the epilogue
     DtpGemmArgs e = a;
@@ -351,6 +400,12 @@ __global__ __launch_bounds__(kThreads) void gemm_ph8_kernel(DtpGemmArgs a) {
   } else {
     store(a);
   }
+  if (!next) break;
+  // the next tile: its prologue parts (and this tile's stores) retired, every wave's
+  // epilogue staging read before the K loop restages buffer 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();
+  }  // for (;;)
 }
 
 // C = alpha * sum_s work[s] + bias (+ C): the epilogue of a split-K launch (f32 out,
@@ -428,6 +483,21 @@ int launch_ph8(const DtpGemmArgs& a, hipStream_t s, int variant) {
   // default (-1): the balanced reads (profiles/gemm_r3_ph8)
   if (variant < 0) variant = 0;
   if ((a.K / 64 / a.splitk) % 2) variant = 2;  // the balanced schedule runs K-tiles in pairs
+  if (variant == 3 && a.splitk == 1) {  // persistent balanced walk: one workgroup per CU (a multiple of 8)
+    int cus = 256, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const long long grid = tiles < cus ? (tiles + 7) / 8 * 8 : cus / 8 * 8;
+    const dim3 gp((unsigned)(grid > 0 ? grid : 8));
+    switch ((a.trans_a ? 2 : 0) | (a.trans_b ? 1 : 0)) {
+      case 0: hipLaunchKernelGGL((ph8::gemm_ph8_kernel<false, false, true, false, true>), gp, b, 0, s, a); break;
+      case 1: hipLaunchKernelGGL((ph8::gemm_ph8_kernel<false, true, true, false, true>), gp, b, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((ph8::gemm_ph8_kernel<true, false, true, false, true>), gp, b, 0, s, a); break;
+      default: hipLaunchKernelGGL((ph8::gemm_ph8_kernel<true, true, true, false, true>), gp, b, 0, s, a); break;
+    }
+    return check_launch("dtp_gemm(8-phase LDS-DMA 256x256, persistent)");
+  }
+  if (variant == 3) variant = 0;
   if (a.splitk > 1) variant == 2 ? launch_lay<false, true>(a, s, g, b) : launch_lay<true, true>(a, s, g, b);
   else variant == 2 ? launch_lay<false, false>(a, s, g, b) : launch_lay<true, false>(a, s, g, b);
   if (a.splitk > 1) {

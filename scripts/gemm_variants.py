@@ -2,8 +2,10 @@
 (cdna_hip_programming.md §5.4 rule 24). usage: python scripts/gemm_variants.py [rounds]
 
 VARIANTS=var2,var32,var34,torch  selects variants (fast = 2 + N): var2 the two-buffer
-kernel, var32 / var34 the 8-phase kernel with balanced / unbalanced reads.
-SHAPES=wide  times the wide-MLP GEMMs (W=4096, batch 8192) instead of the squares."""
+kernel, var32 / var34 the 8-phase kernel with balanced / unbalanced reads, var35 the
+balanced 8-phase kernel as a persistent tile walk.
+SHAPES=wide  times the wide-MLP GEMMs (W=4096, batch 8192) instead of the squares;
+SHAPES=nn the NN per-tile scan."""
 import json
 import os
 import sys
@@ -33,6 +35,9 @@ def main():
     shapes = [(4096, 4096, 4096, "NN"), (8192, 8192, 8192, "NN"), (8192, 8192, 8192, "TT"), (8192, 8192, 8192, "NT")]
     if os.environ.get("SHAPES") == "wide":  # forward, input gradient, weight gradient of a 4096-wide layer
         shapes = [(8192, 4096, 4096, "NN"), (8192, 4096, 4096, "NT"), (4096, 4096, 8192, "TT")]
+    if os.environ.get("SHAPES") == "nn":  # the per-tile cost scan of profiles/r4_gemm (NN, 2-8 tiles per CU)
+        shapes = [(8192, 4096, 2048, "NN"), (8192, 4096, 4096, "NN"), (8192, 4096, 8192, "NN"),
+                  (8192, 8192, 4096, "NN"), (16384, 8192, 4096, "NN"), (8192, 8192, 8192, "NN")]
     for (M, N, K, lay) in shapes:
         ta, tb = lay[0] == "T", lay[1] == "T"
         a = (torch.rand(*((K, M) if ta else (M, K)), device=DEV) * 2 - 1).bfloat16()

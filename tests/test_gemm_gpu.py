@@ -65,7 +65,9 @@ def test_gemm_bf16_big_tile_kernel(ta, tb):
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("shape", [(512, 768, 128), (1000, 1032, 320), (4104, 2056, 192), (1288, 776, 512)])
-@pytest.mark.parametrize("kernel", [True, 4, 34, 36])  # default (8-phase by layout), two-buffer kernel, 8-phase balanced / unbalanced (fast = 2 + variant)
+# default (8-phase by layout), two-buffer kernel, 8-phase balanced / unbalanced, 8-phase
+# persistent tile walk (fast = 2 + variant; odd K-tile counts fall back to the unbalanced one)
+@pytest.mark.parametrize("kernel", [True, 4, 34, 36, 37])
 def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
     """The LDS-DMA 256x256 kernel (row images + transposing LDS reads): every layout,
     ragged M/N edges, bias / LeakyReLU' (aux) epilogues, f32 and bf16 outputs."""
@@ -84,7 +86,7 @@ def test_gemm_bf16_fast_kernel(ta, tb, shape, kernel):
 
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
-@pytest.mark.parametrize("kernel", [True, 4, 34])  # 8-phase default, two-buffer kernel, 8-phase balanced
+@pytest.mark.parametrize("kernel", [True, 4, 34, 37])  # 8-phase default, two-buffer kernel, 8-phase balanced, persistent
 def test_gemm_bf16_fast_kernel_accumulate_epilogues(ta, tb, kernel):
     """Epilogue operands of the LDS-DMA kernel: accumulate into f32 (the in-place weight
     gradient) and bf16 outputs, alpha + bias + LeakyReLU, and an output view whose rows
@@ -328,3 +330,25 @@ def test_compute_shadow_training_is_bit_identical():
     b, sh = run(True)
     assert sh._token == sh._current()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape", [(4104, 4360, 256), (8192, 4096, 128)])  # 17 x 18 tiles (ragged); 512 (XCD remap)
+def test_gemm_persistent_walk_many_tiles_per_workgroup(ta, tb, shape):
+    """The persistent 8-phase kernel with several tiles per workgroup (the next tile's
+    operand fill under this tile's epilogue), ragged edges and a tile count that is not a
+    multiple of 8, or 2 tiles per workgroup through the XCD remap: the same result as the one-tile-per-workgroup balanced kernel, bit for
+    bit (the same K order per output)."""
+    torch.manual_seed(11)
+    M, N, K = shape
+    a = torch.randn(*((K, M) if ta else (M, K)), device="cuda").bfloat16()
+    b = torch.randn(*((K, N) if tb else (N, K)), device="cuda").bfloat16()
+    bias = torch.randn(N, device="cuda")
+    ref = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1, bias=bias, fast=34)
+    got = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32, splitk=1, bias=bias, fast=37)
+    assert torch.equal(ref, got)
+    refb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, act=True, slope=0.1, fast=34)
+    gotb = gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.bfloat16, act=True, slope=0.1, fast=37)
+    assert torch.equal(refb, gotb)
