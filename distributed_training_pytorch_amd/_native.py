@@ -271,6 +271,12 @@ def _declare(lib):
         "dtp_gather_rows2_ring": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_longlong,
                                           c_void_p, c_void_p, c_void_p]),
         "dtp_gather_ring_max_elems": (c_longlong, []),
+        "dtp_format_loss_rows": (c_longlong, [c_void_p, c_int, c_longlong, c_longlong, c_longlong, c_longlong,
+                                              c_longlong, c_int, c_void_p, c_longlong]),
+        "dtp_format_loss_rows_bound": (c_longlong, [c_int, c_longlong]),
+        "dtp_format_loss_rows_jsonl": (c_longlong, [c_void_p, c_int, c_longlong, c_longlong, c_longlong, c_longlong,
+                                                    c_longlong, ctypes.c_char_p, c_void_p, c_longlong]),
+        "dtp_format_loss_rows_jsonl_bound": (c_longlong, [c_int, c_longlong, c_longlong]),
         "dtp_randperm_fill": (c_int, [ctypes.c_ulonglong, c_int, c_longlong, c_int, c_void_p, c_int]),
         "dtp_split_launch": (c_int, [P(SplitLaunch), c_void_p]),
         "dtp_split_shape_id": (c_int, [c_int] * 6),

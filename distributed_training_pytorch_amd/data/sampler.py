@@ -327,7 +327,8 @@ class PermutationRing:
     Slot ``e & (epochs-1)`` holds epoch e's permutation of [0, n): torch's exact
     DistributedSampler order (``kind="torch"``: ``randperm(n)`` seeded with seed+epoch,
     generated by the native MT19937 replica ``csrc/randperm.hip`` on host threads) or
-    the keyed Feistel permutation of the in-kernel device sampler (``kind="feistel"``).
+    the keyed Feistel permutation of the in-kernel device sampler (``kind="feistel"``), or
+    the identity for the unshuffled orders (``kind="identity"``: one slot every epoch reads).
     The fused train kernel reads a lane's dataset index from the ring a step ahead,
     so the reference's exact sample order costs no host work per step.
 
@@ -340,13 +341,18 @@ class PermutationRing:
                  budget_ints: int = 1 << 24):
         import threading
 
-        if kind not in ("torch", "feistel"):
-            raise ValueError(f"permutation kind {kind!r}: torch or feistel")
+        if kind not in ("torch", "feistel", "identity"):
+            raise ValueError(f"permutation kind {kind!r}: torch, feistel or identity")
         self.geom = geom
         self.n = geom.n
         self.kind = kind
         self.device = torch.device(device)
-        if epochs is None:
+        if kind == "identity":
+            # the unshuffled orders (DistributedSampler(shuffle=False), or one rank reading the
+            # dataset in order) as one identity "permutation" every epoch shares: the fused
+            # step's FAST sampler path then serves them too (it reads a SAMPLER_TABLE ring)
+            epochs = 1
+        elif epochs is None:
             epochs = max(2, min(8192, budget_ints // max(self.n, 1)))
         self.E = 1 << (int(epochs).bit_length() - 1)  # power of two
         self.table = torch.empty(self.E, self.n, dtype=torch.int32, device=self.device)
@@ -360,7 +366,9 @@ class PermutationRing:
     # ---------------------------------------------------------------- generation
     def _generate(self, e0: int, count: int) -> torch.Tensor:
         host = torch.empty(count, self.n, dtype=torch.int32, pin_memory=self.device.type == "cuda")
-        if self.kind == "torch":
+        if self.kind == "identity":
+            host.copy_(torch.arange(self.n, dtype=torch.int32).expand(count, self.n))
+        elif self.kind == "torch":
             self._fill_torch(e0, count, host)
         else:
             for k in range(count):
@@ -425,6 +433,8 @@ class PermutationRing:
         return e_lo < self.lo or e_hi > self.hi
 
     def ensure(self, e_lo: int, e_hi: int) -> None:
+        if self.kind == "identity":  # every epoch is the one resident table
+            return
         if e_hi - e_lo + 1 > self.E:
             raise ValueError(f"a launch spanning {e_hi - e_lo + 1} epochs exceeds the {self.E}-epoch ring: "
                              "launch fewer steps at a time")

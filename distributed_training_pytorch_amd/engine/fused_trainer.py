@@ -29,7 +29,8 @@ import torch.distributed as dist
 
 from .. import _native as nat
 from ..parallel import comm_util
-from ..data.sampler import SAMPLER_DIST_SHUFFLE, EpochIndexStream, PermutationRing, SamplerGeometry
+from ..data.sampler import (SAMPLER_DIST_NOSHUFFLE, SAMPLER_DIST_SHUFFLE, SAMPLER_SEQUENTIAL, EpochIndexStream,
+                             PermutationRing, SamplerGeometry)
 from ..ops.mlp import MlpSpec, mlp_forward_ref
 from ..ops.optim import OptimConfig, adam_update_ref, flat_optimizer_step, sgd_update_ref
 
@@ -129,6 +130,10 @@ class FusedTrainer:
                 if self.cfg.sampler not in ("torch", "device"):
                     raise ValueError(f"sampler {self.cfg.sampler!r}: torch or device")
                 self._ring = PermutationRing(geom, dev, kind="torch" if self.cfg.sampler == "torch" else "feistel")
+            elif geom.mode == SAMPLER_DIST_NOSHUFFLE or (geom.mode == SAMPLER_SEQUENTIAL and geom.world == 1):
+                # an unshuffled order as an identity table: the same indices, and the fast
+                # step instances (which read a SAMPLER_TABLE ring) instead of the generic one
+                self._ring = PermutationRing(geom, dev, kind="identity")
         if self.comm == "xgmi":
             self._setup_xgmi()
 
@@ -648,9 +653,13 @@ class LossReadback:
         self.rows, self.status, self.event, self.rank = rows, status, event, rank
 
     def wait(self) -> list[list[float]]:
+        return self.wait_tensor().tolist()
+
+    def wait_tensor(self) -> torch.Tensor:
+        """The rows as the host tensor they were copied into ([steps, n_models] fp32)."""
         if self.event is not None:
             self.event.synchronize()
         if self.status is not None and int(self.status[0]):
             raise RuntimeError(f"xGMI exchange timed out on rank {self.rank} at epoch {int(self.status[1])} "
                                "(peer not responding)")
-        return self.rows.tolist()
+        return self.rows

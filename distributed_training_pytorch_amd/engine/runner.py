@@ -190,7 +190,7 @@ def _train_fused(config, device, rank, world, logger, faults) -> dict:
     def process(p):
         it0, n, handle = p
         with timer.phase("loss_readback"):
-            ls = handle.wait()  # raises on a sticky xGMI timeout: never train on partial sums
+            ls = handle.wait_tensor()  # raises on a sticky xGMI timeout: never train on partial sums
         logger.log_rows(list(range(it0, it0 + n)), ["loss/lossX", "loss/lossY"], ls[:n])
         if pbar is not None:
             pbar.update(n)

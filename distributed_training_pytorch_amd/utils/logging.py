@@ -62,12 +62,26 @@ class MetricLogger:
         if commit:
             self.step = step + 1
 
-    def log_rows(self, steps: list[int], names: list[str], rows: list[list[float]]) -> None:
+    def log_rows(self, steps: list[int], names: list[str], rows) -> None:
         """A block of per-step metrics in one call (the fused engines read their losses
         back once per launch): the same rows ``log`` writes -- one wandb row per step
-        with every name, one JSONL line per step -- built as one string and written once."""
+        with every name, one JSONL line per step -- built as one string and written once.
+        ``rows``: lists, or a host fp32 tensor [len(steps), len(names)] whose JSONL text
+        the native formatter builds (``csrc/host_log.hip``, json.dumps' exact spelling)
+        for consecutive steps."""
         if not self.enabled or not steps:
             return
+        import torch
+
+        if isinstance(rows, torch.Tensor):
+            t = rows.detach()
+            if (self._wandb is None and self._f is not None and t.device.type == "cpu" and t.dtype == torch.float32
+                    and t.dim() == 2 and t.is_contiguous() and tuple(t.shape) == (len(steps), len(names))
+                    and list(steps) == list(range(steps[0], steps[0] + len(steps)))):
+                if self._write_native(steps[0], names, t):
+                    self.step = steps[-1] + 1
+                    return
+            rows = t.tolist()
         if self._wandb is not None:
             for st, row in zip(steps, rows):
                 self._wandb.log(dict(zip(names, map(float, row))), step=st)
@@ -81,6 +95,24 @@ class MetricLogger:
             self._f.write("".join('{"step": %d, %s}\n' % (st, ", ".join("%s: %s" % (k, num(v)) for k, v in zip(keys, row)))
                                   for st, row in zip(steps, rows)))
         self.step = steps[-1] + 1
+
+    def _write_native(self, step0: int, names, t) -> bool:
+        import ctypes
+        import json as _json
+
+        from .. import _native as nat
+
+        if not nat.native_enabled() or os.environ.get("DTP_NATIVE_LOG", "1") == "0":  # (A/B switch)
+            return False
+        lib = nat.load()
+        keys = "".join(_json.dumps(k) + "\n" for k in names).encode()
+        cap = lib.dtp_format_loss_rows_jsonl_bound(len(names), t.shape[0], len(keys))
+        buf = ctypes.create_string_buffer(cap)
+        m = lib.dtp_format_loss_rows_jsonl(t.data_ptr(), len(names), 0, t.shape[0], 1, step0, 1, keys, buf, cap)
+        if m < 0:
+            return False
+        self._f.write(buf.raw[:m].decode("utf-8"))
+        return True
 
     def finish(self) -> None:
         if not self.enabled:

@@ -252,3 +252,25 @@ def test_split_batch_dead_launch_keeps_the_state():
     with pytest.raises(RuntimeError, match="timed out"):
         tr.check_comm()
     tr.close()
+
+
+@pytest.mark.parametrize("distributed", [True, False], ids=["dist_noshuffle", "sequential"])
+def test_unshuffled_orders_take_the_fast_step_and_match_torch(distributed):
+    """DistributedSampler(shuffle=False) and one rank reading the dataset in order (the
+    Lightning demo at one GPU) go through an identity permutation table, so the fast step
+    instances serve them (they read a SAMPLER_TABLE ring): the same order and results as
+    autograd + torch.optim on those indices."""
+    X, Y = ToyData(n=512, seed=21).device_tensors(DEV)
+    geom = SamplerGeometry(n=512, batch=128, seed=3, shuffle=False, distributed=distributed)
+    init = _init(TOY_SPEC, 77)
+    ocfg = OptimConfig(lr=1e-2)
+    tr = FusedTrainer(TOY_SPEC, 2, X, Y, geom, ocfg, EngineConfig(steps_per_launch=7), init_params=init)
+    assert tr._ring is not None and tr._ring.kind == "identity"
+    assert tr.lanes > 1  # a several-lanes / split-batch instance, not the generic one-lane step
+    steps = 3 * geom.steps_per_epoch + 1
+    tr.train(steps)
+    tr.synchronize()
+    ref_p, ref_l = torch_train(TOY_SPEC, init, X, Y, [EpochIndexStream(geom)], steps, ocfg)
+    torch.testing.assert_close(tr.losses(0, steps), ref_l, rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(tr.params.cpu(), ref_p, rtol=1e-4, atol=2e-5)
+    tr.close()
