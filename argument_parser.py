@@ -48,12 +48,15 @@ def build_parser(description: str | None = None) -> argparse.ArgumentParser:
                         "fused kernels per op; stock: plain PyTorch eager DDP (the comparison baseline)")
     p.add_argument("--comm", choices=["auto", "rccl", "xgmi", "host"], default="auto")
     p.add_argument("--launch", choices=["persistent", "graph", "eager"], default="persistent")
-    p.add_argument("--steps_per_launch", type=int, default=50,
+    # 200: a launch's ~15 us of launch + completion spread over 200 steps (50: 67.5 M samples/s
+    # on the fused engine, profiles/r6_native_log/); every step is still logged, one block per launch
+    p.add_argument("--steps_per_launch", type=int, default=200,
                    help="iterations per kernel launch / graph (also the host logging granularity)")
     p.add_argument("--sampler", choices=["torch", "device"], default="torch",
                    help="torch: the reference's exact DistributedSampler order (randperm per epoch, read by "
                         "the kernels from a device ring the host fills ahead); device: keyed Feistel shuffle")
-    p.add_argument("--log_every", type=int, default=50)
+    p.add_argument("--log_every", type=int, default=200,
+                   help="steps per host read-back of the per-step losses (each step is still logged)")
     p.add_argument("--log_dir", type=str, default=None)
     p.add_argument("--project", type=str, default="distributed tester")
     p.add_argument("--checkpoint_dir", type=str, default=None)
