@@ -364,7 +364,16 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
             and os.environ.get("DTP_MODULE_RING", "1") != "0"):
         epoch_ring = torch.zeros(1 + geom.steps_per_epoch * geom.batch, dtype=torch.int64, device=device)
         epoch_ring[0] = geom.batch_pos(start)[1] // geom.batch  # the cursor: the first step's batch in its epoch
+    # steady-state clock (the summary's steady_samples_per_s): from the end of step
+    # steady_from on -- the first kernels' code-object loads, the warm-up runs and the
+    # graph captures fall before it (they are a fixed cost that dominates short runs and
+    # varies by box); synchronised at both ends
+    steady_from = start + min(50, (config.iters - start) // 2)
+    t_steady = None
     for it in range(start, config.iters):
+        if it == steady_from and device.type == "cuda":
+            torch.cuda.synchronize(device)
+            t_steady = time.perf_counter()
         faults.check(it)
         size = geom.batch_size_at(it)
         if epoch_ring is not None:
@@ -391,7 +400,11 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     ddp.check_comm()
-    dt = time.perf_counter() - t0
+    t_end = time.perf_counter()
+    dt = t_end - t0
+    steady = None
+    if t_steady is not None and config.iters > steady_from:
+        steady = geom.batch * (config.iters - steady_from) * world / max(t_end - t_steady, 1e-9)
     if pbar is not None:
         pbar.close()
     if config.check_replicas:
@@ -399,7 +412,8 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     if config.checkpoint_dir:
         _save(config.iters)
     return {"final_loss": last, "iters": config.iters,
-            "samples_per_s": geom.batch * (config.iters - start) * world / max(dt, 1e-9), "engine": "module",
+            "samples_per_s": geom.batch * (config.iters - start) * world / max(dt, 1e-9),
+            "steady_samples_per_s": steady, "engine": "module",
             "graph_replays": stepper.replays,
             **({"phases": timer.summary()} if trace_enabled() else {})}
 
