@@ -271,6 +271,8 @@ def _declare(lib):
         "dtp_gather_rows2_ring": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_longlong,
                                           c_void_p, c_void_p, c_void_p]),
         "dtp_gather_ring_max_elems": (c_longlong, []),
+        "dtp_gather_rows2_sampler": (c_int, [c_void_p, c_int, c_void_p, c_int, P(SamplerCfg), c_void_p, c_int,
+                                             c_longlong, c_void_p, c_void_p, c_void_p]),
         "dtp_format_loss_rows": (c_longlong, [c_void_p, c_int, c_longlong, c_longlong, c_longlong, c_longlong,
                                               c_longlong, c_int, c_void_p, c_longlong]),
         "dtp_format_loss_rows_bound": (c_longlong, [c_int, c_longlong]),

@@ -159,9 +159,55 @@ __global__ __launch_bounds__(kBlock) void gather_rows2_ring_kernel(const float* 
   if (threadIdx.x == 0) ring[0] = cur + 1;
 }
 
+// the same gather with the indices computed on the device by the engine's sampler
+// (sampler.h: batch_pos + sample_index -- DistributedSampler order from the device
+// permutation ring (SAMPLER_TABLE), the keyed shuffle, or the unshuffled orders) for step
+// cursor[0], which the kernel advances: a replayed step draws its batch with no index
+// buffer refreshed by the host at all, not even per epoch.  ONE workgroup.
+__global__ __launch_bounds__(kBlock) void gather_rows2_sampler_kernel(const float* __restrict__ X, int dx,
+                                                                      const float* __restrict__ Y, int dy,
+                                                                      SamplerCfg smp, long long* __restrict__ cursor,
+                                                                      int n, long long nrows, float* __restrict__ ox,
+                                                                      float* __restrict__ oy) {
+  __shared__ int sidx[kBlock * 4];
+  const long long t = cursor[0];
+  const BatchPos bp = batch_pos(smp, t);
+  uint32_t keys[4] = {0u, 0u, 0u, 0u};
+  if (smp.mode == SAMPLER_DIST_SHUFFLE) epoch_keys(smp, bp.epoch, keys);
+  const int m = n < bp.size ? n : bp.size;
+  for (int r = threadIdx.x; r < m; r += kBlock) {
+    int s = sample_index(smp, bp, keys, r);
+    s = s < 0 ? 0 : (s >= nrows ? (int)(nrows - 1) : s);
+    sidx[r] = s;
+  }
+  __syncthreads();
+  const int w = dx + dy;
+  for (int i = threadIdx.x; i < m * w; i += kBlock) {
+    const int r = i / w, c = i - r * w;
+    const long long s = sidx[r];
+    if (c < dx) ox[(long long)r * dx + c] = X[s * dx + c];
+    else oy[(long long)r * dy + (c - dx)] = Y[s * dy + (c - dx)];
+  }
+  if (threadIdx.x == 0) cursor[0] = t + 1;  // every thread read the cursor before the barrier
+}
+
 }  // namespace dtp
 
 extern "C" {
+
+long long dtp_gather_ring_max_elems();
+
+int dtp_gather_rows2_sampler(const float* X, int dx, const float* Y, int dy, const dtp::SamplerCfg* smp,
+                             long long* cursor, int n, long long nrows, float* ox, float* oy, void* stream) {
+  if (!X || !Y || !smp || !cursor || !ox || !oy || n <= 0 || n > 4 * dtp::kBlock || dx <= 0 || dy <= 0 ||
+      nrows <= 0 || smp->batch <= 0 || smp->steps_per_epoch <= 0 || smp->n != nrows ||
+      (long long)n * (dx + dy) > dtp_gather_ring_max_elems() ||
+      (smp->mode == dtp::SAMPLER_TABLE && (!smp->perm || smp->perm_epochs <= 0)))
+    return dtp::set_err(-1, "gather_rows2_sampler: bad arguments");
+  hipLaunchKernelGGL(dtp::gather_rows2_sampler_kernel, dim3(1), dim3(dtp::kBlock), 0, (hipStream_t)stream, X, dx, Y,
+                     dy, *smp, cursor, n, nrows, ox, oy);
+  return dtp::check_launch("gather_rows2_sampler_kernel");
+}
 
 // one workgroup streams at most this many gathered elements per launch (the toy batches
 // are a few hundred); larger batches take the host-refreshed index path

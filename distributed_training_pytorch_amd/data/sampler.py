@@ -250,6 +250,17 @@ class BatchIndexer:
                 self._cfg = geom.to_native()
                 self._buf = torch.empty(self.block, geom.batch, dtype=torch.int32, device=self.device)
 
+    def permutation_ring(self):
+        """The device ``PermutationRing`` this indexer reads (DistributedSampler's exact
+        shuffled order on a GPU), or None."""
+        return self._ring
+
+    def needs_ring(self) -> bool:
+        """Whether the order needs a permutation table the native sampler cannot compute
+        itself: torch's exact shuffled order (the keyed Feistel order and the unshuffled
+        orders are computed on the device from the step number)."""
+        return self.exact and self.geom.distributed and self.geom.shuffle
+
     def can_fill_epoch(self) -> bool:
         """Whether ``epoch_into`` is available (the device permutation ring or the host
         epoch list; not the native per-step sampler's blocks)."""

@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from ..data.sampler import BatchIndexer, SamplerGeometry
 from ..data.toy_data import ToyData
-from ..ops.gather import gather_rows2, gather_rows2_ring, ring_gather_ok
+from ..ops.gather import gather_rows2, gather_rows2_ring, gather_rows2_sampler, ring_gather_ok
 from ..ops.loss import MSELoss
 from ..ops.mlp import ParamBackwardFusion
 from ..ops.optim import OptimConfig
@@ -318,7 +318,9 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
             if size not in xb:
                 xb[size] = (torch.empty(size, X.shape[1], device=device), torch.empty(size, Y.shape[1], device=device))
             x, y = xb[size]
-            if epoch_ring is not None:  # indices from the device epoch ring, cursor advanced on the device
+            if samp_cfg is not None:  # indices from the device sampler, step cursor advanced on the device
+                gather_rows2_sampler(X, Y, samp_cfg, samp_cursor, x, y)
+            elif epoch_ring is not None:  # indices from the device epoch ring, cursor advanced on the device
                 gather_rows2_ring(X, Y, epoch_ring, geom.batch, geom.steps_per_epoch, x, y)
             else:
                 gather_rows2(X, Y, idx_static[:size], x, y)  # both tensors in one launch
@@ -359,9 +361,21 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
     stepper = CapturedStep(step_body, device, enabled=graphable, on_abort=_abort)
     # the device epoch ring {cursor, the epoch's indices} of the replayed step's gather: one
     # fill per epoch instead of an index copy per step (DTP_MODULE_RING=0: the copies, A/B)
+    # better still, the step's indices computed on the device by the engine's own sampler
+    # (sampler.h, reading the device permutation ring for DistributedSampler's exact order):
+    # no host index work per epoch either (DTP_MODULE_RING=epoch: the epoch ring, A/B)
     epoch_ring, ring_epoch = None, None
-    if (graphable and indexer.can_fill_epoch() and ring_gather_ok(X, Y, geom.batch)
-            and os.environ.get("DTP_MODULE_RING", "1") != "0"):
+    samp_cfg, samp_cursor, perm_ring = None, None, None
+    ring_mode = os.environ.get("DTP_MODULE_RING", "sampler")
+    if graphable and ring_gather_ok(X, Y, geom.batch) and ring_mode == "sampler" and geom.batch <= 1024:
+        perm_ring = indexer.permutation_ring()
+        if perm_ring is not None or not indexer.needs_ring():
+            samp_cfg = geom.to_native()
+            if perm_ring is not None:
+                perm_ring.native(samp_cfg)
+            samp_cursor = torch.full((1,), start, dtype=torch.int64, device=device)
+    if (samp_cfg is None and graphable and indexer.can_fill_epoch() and ring_gather_ok(X, Y, geom.batch)
+            and ring_mode != "0"):
         epoch_ring = torch.zeros(1 + geom.steps_per_epoch * geom.batch, dtype=torch.int64, device=device)
         epoch_ring[0] = geom.batch_pos(start)[1] // geom.batch  # the cursor: the first step's batch in its epoch
     # steady-state clock (the summary's steady_samples_per_s): from the end of step
@@ -376,7 +390,12 @@ def _train_module(config, device, rank, world, logger, faults) -> dict:
             t_steady = time.perf_counter()
         faults.check(it)
         size = geom.batch_size_at(it)
-        if epoch_ring is not None:
+        if samp_cfg is not None:
+            ep = geom.batch_pos(it)[0]
+            if perm_ring is not None and ep != ring_epoch:  # resident before the replay that reads it
+                perm_ring.ensure(ep, ep)
+                ring_epoch = ep
+        elif epoch_ring is not None:
             ep = geom.batch_pos(it)[0]
             if ep != ring_epoch:  # stream-ordered after the last replay that read the old epoch
                 indexer.epoch_into(ep, epoch_ring[1:1 + geom.num_samples])

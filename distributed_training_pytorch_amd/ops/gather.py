@@ -56,3 +56,20 @@ def gather_rows2_ring(X: torch.Tensor, Y: torch.Tensor, ring: torch.Tensor, batc
     torch.index_select(X, 0, idx, out=ox)
     torch.index_select(Y, 0, idx, out=oy)
     ring[0] += 1
+
+
+def gather_rows2_sampler(X: torch.Tensor, Y: torch.Tensor, cfg, cursor: torch.Tensor, ox: torch.Tensor,
+                         oy: torch.Tensor) -> None:
+    """Gather the batch of step ``cursor[0]`` as the engine's sampler orders it (``cfg``: a
+    ``SamplerCfg``, pointed at a device permutation ring for DistributedSampler's exact
+    order) into ``ox`` / ``oy`` and advance ``cursor[0]`` -- indices and gather in one
+    launch on the device (``gather_rows2_sampler_kernel``); no host index work per step or
+    epoch.  GPU only (the engines call it where ``ring_gather_ok`` holds)."""
+    n = ox.shape[0]
+    if not (cursor.is_cuda and cursor.dtype == torch.int64 and _native_ok(X, Y, ox, oy, n)):
+        raise RuntimeError("gather_rows2_sampler: fp32 CUDA data, an int64 CUDA cursor and the native library")
+    import ctypes
+
+    nat.check(nat.load().dtp_gather_rows2_sampler(nat.ptr(X), X.shape[1], nat.ptr(Y), Y.shape[1], ctypes.byref(cfg),
+                                                  nat.ptr(cursor), n, X.shape[0], nat.ptr(ox), nat.ptr(oy),
+                                                  nat.stream_ptr()), "dtp_gather_rows2_sampler")

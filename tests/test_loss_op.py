@@ -253,3 +253,60 @@ def test_mse_loss_pair_log_cpu_form():
     a1, a2, b = torch.randn(8, 1), torch.randn(8, 1), torch.randn(8, 1)
     l1, l2, _ = mse_loss_pair(a1, a2, b, log=(rows, slot))
     assert int(slot) == 2 and rows[1, 0] == l1 and rows[1, 1] == l2 and not rows[0].any() and not rows[2].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["torch_shuffle", "device_shuffle", "noshuffle", "sequential"])
+def test_sampler_gather_follows_the_batch_indexer(mode):
+    """gather_rows2_sampler: the step's indices computed on the device by the engine's
+    sampler (torch's exact DistributedSampler order from the device permutation ring, the
+    keyed shuffle, the unshuffled orders), the cursor advanced by the kernel -- the same
+    rows as the host-side BatchIndexer, step after step across epochs and short batches,
+    also when replayed from a captured graph."""
+    from distributed_training_pytorch_amd import _native as nat
+    from distributed_training_pytorch_amd.data.sampler import BatchIndexer, SamplerGeometry
+    from distributed_training_pytorch_amd.ops.gather import gather_rows2_sampler
+
+    nat.require(torch.device("cuda", 0))
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(500, 2, generator=g).cuda()
+    Y = torch.randn(500, 1, generator=g).cuda()
+    geom = SamplerGeometry(n=500, world=2, rank=1, batch=96, seed=4, shuffle=mode.endswith("shuffle") and
+                           mode != "noshuffle", distributed=mode != "sequential")
+    exact = mode != "device_shuffle"
+    ref = BatchIndexer(geom, torch.device("cuda", 0), exact_torch=exact)
+    dev_ix = BatchIndexer(geom, torch.device("cuda", 0), exact_torch=exact)
+    cfg = geom.to_native()
+    ring = dev_ix.permutation_ring()
+    assert (ring is not None) == dev_ix.needs_ring()
+    if ring is not None:
+        ring.native(cfg)
+    cursor = torch.full((1,), 3, dtype=torch.int64, device="cuda")
+    steps = 3 * geom.steps_per_epoch + 2
+    for t in range(3, steps):
+        if ring is not None:
+            e = geom.batch_pos(t)[0]
+            ring.ensure(e, e)
+        size = geom.batch_size_at(t)
+        ox, oy = torch.empty(size, 2, device="cuda"), torch.empty(size, 1, device="cuda")
+        gather_rows2_sampler(X, Y, cfg, cursor, ox, oy)
+        idx = ref(t).long()
+        assert torch.equal(ox, X[idx]) and torch.equal(oy, Y[idx]), t
+    assert int(cursor) == steps
+    # replayed: a captured gather draws the next step's batch every replay
+    t = steps
+    while geom.batch_size_at(t) != geom.batch:
+        t += 1
+    cursor.fill_(t)
+    ox, oy = torch.empty(geom.batch, 2, device="cuda"), torch.empty(geom.batch, 1, device="cuda")
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    if ring is not None:
+        ring.ensure(geom.batch_pos(t)[0], geom.batch_pos(t)[0] + 1)
+    with torch.cuda.graph(gr, stream=s):
+        gather_rows2_sampler(X, Y, cfg, cursor, ox, oy)
+    gr.replay()
+    torch.cuda.synchronize()
+    idx = ref(t).long()
+    assert torch.equal(ox, X[idx]) and int(cursor) == t + 1
