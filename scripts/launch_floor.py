@@ -23,12 +23,16 @@ from distributed_training_pytorch_amd.models.toy import ToyModel  # noqa: E402
 from distributed_training_pytorch_amd.ops.mlp import TOY_SPEC  # noqa: E402
 
 
-def med(fn, reps=300):
+def med(fn, reps=300, pre_sync=None):
+    """pre_sync: called before the closing torch.cuda.synchronize (e.g. the stream's own
+    synchronize: whether waiting on the stream first shortens the device-wide wait)."""
     ts = []
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         fn()
+        if pre_sync is not None:
+            pre_sync()
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e6)
     return round(statistics.median(ts), 2)
@@ -49,6 +53,10 @@ def main():
         out = {"sync": med(lambda: None), "torch_tiny": med(lambda: x.add_(1.0))}
         for k in (1, 20, 200):
             out[f"train_{k}"] = med(lambda k=k: tr.train(k), reps=100 if k == 200 else 300)
+        out["train_20_stream_sync_first"] = med(lambda: tr.train(20), pre_sync=s.synchronize)
+        ev = torch.cuda.Event()
+        out["train_20_event_sync_first"] = med(lambda: (tr.train(20), ev.record(s)), pre_sync=ev.synchronize)
+        out["train_20_again"] = med(lambda: tr.train(20))
         tr.close()
     out["per_step_slope_us"] = round((out["train_200"] - out["train_20"]) / 180, 3)
     out["fixed_us"] = round(out["train_20"] - 20 * out["per_step_slope_us"], 2)
