@@ -57,6 +57,25 @@ def main():
         ev = torch.cuda.Event()
         out["train_20_event_sync_first"] = med(lambda: (tr.train(20), ev.record(s)), pre_sync=ev.synchronize)
         out["train_20_again"] = med(lambda: tr.train(20))
+        # the host's side alone: time to return from train(20) (enqueue), and from the bare
+        # native call it ends in (same arguments, no Python bookkeeping)
+        def host_only(fn, reps=300):
+            ts = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                ts.append((time.perf_counter() - t0) * 1e6)
+                torch.cuda.synchronize()
+            return round(statistics.median(ts), 2)
+
+        out["host_train_20"] = host_only(lambda: tr.train(20))
+        e, run, di = tr._engine_handle(), tr._engine_run, tr._dev_index
+
+        def bare():
+            run(e, 20, tr.t, nat.raw_stream(di))
+            tr.t += 20
+        out["host_bare_engine_run_20"] = host_only(bare)
         tr.close()
     out["per_step_slope_us"] = round((out["train_200"] - out["train_20"]) / 180, 3)
     out["fixed_us"] = round(out["train_20"] - 20 * out["per_step_slope_us"], 2)
